@@ -1,0 +1,234 @@
+/*
+ * policygpu -- MI355X-native network-policy classification engine for Contiv-VPP.
+ *
+ * C ABI (the cgo boundary). Every entry point takes plain pointers and sizes; nothing here
+ * retains a caller pointer after it returns (cgo pointer-passing rules). All calls are
+ * synchronous from the caller's point of view unless a hip stream is passed, and a context
+ * is not re-entrant (the reference drives the renderer from one event-loop goroutine,
+ * plugins/controller/plugin_controller.go:428).
+ *
+ * Reference interfaces replaced (file:line under itaimlx/vpp):
+ *   renderer.PolicyRendererAPI.NewTxn        plugins/policy/renderer/api.go:33-41
+ *   renderer.Txn.Render / Txn.Commit         plugins/policy/renderer/api.go:44-61
+ *   renderer.ContivRule                      plugins/policy/renderer/api.go:65-77
+ *   acl.Renderer (Init/NewTxn/Commit)        plugins/policy/renderer/acl/acl_renderer.go:93-250
+ *   MockACLEngine.ApplyTxn/PutACL/DelACL     mock/aclengine/aclengine_mock.go:151-228, 664-712
+ *   MockACLEngine.RegisterPod                mock/aclengine/aclengine_mock.go:144-148
+ *   MockACLEngine.Connection*                mock/aclengine/aclengine_mock.go:273-420
+ *   MockACLEngine.evalACL / testConnection   mock/aclengine/aclengine_mock.go:424-652 (device)
+ *   ipv4net.API getters used by the path     mock/ipv4net/ipv4net_mock.go:70-110
+ *   contivconf main/other interfaces         plugins/policy/renderer/acl/acl_renderer.go:70-79
+ *   statscollector.RegisterGaugeFunc sink    plugins/statscollector/plugin_impl_statscollector.go:248-261
+ *                                            (pg_read_counters is the pull-style value source)
+ */
+#ifndef POLICYGPU_H
+#define POLICYGPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes (negative errno style) ---------------------------------------- */
+#define PG_OK 0
+#define PG_ENOENT (-2)    /* unknown pod / ACL / interface                               */
+#define PG_EIO (-5)       /* HIP runtime error                                           */
+#define PG_ENOMEM (-12)   /* host or device allocation failed                            */
+#define PG_EINVAL (-22)   /* invalid argument                                            */
+#define PG_EFAULT (-14)   /* the operation failed the way the reference's would (Commit / ApplyTxn error) */
+
+/* ---- enums: values identical to the reference ------------------------------------ */
+enum { PG_ACTION_DENY = 0, PG_ACTION_PERMIT = 1 };                 /* renderer.ActionType    */
+enum { PG_PROTO_TCP = 0, PG_PROTO_UDP = 1, PG_PROTO_OTHER = 2, PG_PROTO_ANY = 3 }; /* ProtocolType */
+enum { PG_ACL_DENY = 0, PG_ACL_PERMIT = 1, PG_ACL_REFLECT = 2, PG_ACL_FAILURE = 3 }; /* ACLAction */
+enum { PG_CONN_DENY_SYN = 0, PG_CONN_DENY_SYN_ACK = 1, PG_CONN_ALLOW = 2, PG_CONN_FAILURE = 3 };
+enum { PG_ORIENT_INGRESS = 0, PG_ORIENT_EGRESS = 1 };             /* cache.Orientation      */
+
+/* net.IPNet: family 0 = empty network (&net.IPNet{}, "match all"), 4 or 6.
+ * addr is the *unmasked* address as the caller holds it (IPv4 in addr[0..3]);
+ * prefix_len is the mask's ones (net.CIDRMask(prefix_len, 32|128)).                    */
+typedef struct pg_ipnet {
+    uint8_t family;
+    uint8_t prefix_len;
+    uint8_t _pad[2];
+    uint8_t addr[16];
+} pg_ipnet;
+
+/* renderer.ContivRule */
+typedef struct pg_contiv_rule {
+    int32_t action;    /* PG_ACTION_*  */
+    int32_t protocol;  /* PG_PROTO_*   */
+    uint16_t src_port; /* 0 = any      */
+    uint16_t dst_port; /* 0 = any      */
+    pg_ipnet src;
+    pg_ipnet dst;
+} pg_contiv_rule;
+
+/* ---- vpp_acl.ACL wire model (vendor/github.com/ligato/vpp-agent/api/models/vpp/acl/acl.proto:24-113)
+ * Strings are CIDRs as rendered by the reference ("" = field unset).                   */
+typedef struct pg_port_range {
+    uint32_t lower_port;
+    uint32_t upper_port;
+} pg_port_range;
+
+typedef struct pg_l4 {
+    uint8_t present;       /* section exists (ipRule.Tcp / ipRule.Udp != nil) */
+    uint8_t has_src_range; /* SourcePortRange != nil                          */
+    uint8_t has_dst_range; /* DestinationPortRange != nil                     */
+    uint8_t _pad;
+    pg_port_range src_range;
+    pg_port_range dst_range;
+} pg_l4;
+
+typedef struct pg_acl_rule {
+    int32_t action; /* vpp_acl.ACL_Rule_Action: 0 DENY, 1 PERMIT, 2 REFLECT */
+    uint8_t has_macip_rule;
+    uint8_t has_ip_rule;
+    uint8_t has_ip;
+    uint8_t has_icmp;
+    const char* src_network;
+    const char* dst_network;
+    pg_l4 tcp;
+    pg_l4 udp;
+} pg_acl_rule;
+
+typedef struct pg_acl {
+    const char* name;
+    const pg_acl_rule* rules;
+    size_t n_rules;
+    const char* const* ingress; /* Interfaces.Ingress */
+    size_t n_ingress;
+    const char* const* egress;  /* Interfaces.Egress  */
+    size_t n_egress;
+} pg_acl;
+
+typedef struct pg_acl_op {
+    const char* key;     /* "config/vpp/acls/v2/acl/<name>" (vpp_acl.Key) */
+    const pg_acl* value; /* NULL = delete                                  */
+} pg_acl_op;
+
+/* ---- tuples (device pointers, SoA) ------------------------------------------------- */
+typedef struct pg_tuple_soa {
+    const uint32_t* src_ip;   /* host-order IPv4                      */
+    const uint32_t* dst_ip;
+    const uint16_t* src_port; /* only read by PG_MODE_CONN            */
+    const uint16_t* dst_port;
+    const uint8_t* proto;     /* PG_PROTO_*                           */
+} pg_tuple_soa;
+
+/* Classification modes.
+ *  SINGLE: evalACL(table, src, dst, proto, dport) for one table         (configs 1,2,4)
+ *  PERPOD: evalACL(outbound ACL of the interface the packet leaves by --
+ *          dst pod's TAP or the node-output interface)                  (config 3)
+ *  CONN:   testConnection over the src/dst interfaces resolved by IP    (config 5)
+ * Output word: bits 31-30 = ACLAction (SINGLE/PERPOD) or ConnAction (CONN),
+ *              bits 29-0  = counter slot of the deciding rule (see pg_num_counter_slots). */
+enum { PG_MODE_SINGLE = 0, PG_MODE_PERPOD = 1, PG_MODE_CONN = 2 };
+#define PG_VERDICT_ACTION(w) ((uint32_t)(w) >> 30)
+#define PG_VERDICT_SLOT(w) ((uint32_t)(w)&0x3FFFFFFFu)
+
+/* ---- engine context (one GPU) ------------------------------------------------------ */
+typedef struct pg_ctx pg_ctx;
+typedef struct pg_renderer pg_renderer;
+typedef struct pg_txn pg_txn;
+
+pg_ctx* pg_create(int hip_device);
+void pg_destroy(pg_ctx* ctx);
+const char* pg_last_error(const pg_ctx* ctx);
+const char* pg_version(void);
+
+/* ipv4net / contivconf roles the renderer and the engine depend on */
+int pg_set_pod_if_name(pg_ctx* ctx, const char* pod_namespace, const char* pod_name, const char* if_name);
+int pg_set_host_interconnect_if_name(pg_ctx* ctx, const char* if_name);
+int pg_set_main_interface_name(pg_ctx* ctx, const char* if_name);
+int pg_set_other_vpp_interfaces(pg_ctx* ctx, const char* const* if_names, size_t n);
+int pg_set_vxlan_bvi_if_name(pg_ctx* ctx, const char* if_name);
+/* MockACLEngine.RegisterPod */
+int pg_register_pod(pg_ctx* ctx, const char* pod_namespace, const char* pod_name, const char* ip, int another_node);
+
+/* ---- renderer (PolicyRendererAPI) -------------------------------------------------- */
+pg_renderer* pg_renderer_new(pg_ctx* ctx, int orientation);
+void pg_renderer_free(pg_renderer* r);
+pg_txn* pg_renderer_new_txn(pg_renderer* r, int resync);
+int pg_txn_render(pg_txn* txn, const char* pod_namespace, const char* pod_name, const pg_ipnet* pod_ip,
+                  const pg_contiv_rule* ingress, size_t n_ingress, const pg_contiv_rule* egress, size_t n_egress,
+                  int removed);
+int pg_txn_commit(pg_txn* txn); /* renders, applies to the engine, frees txn */
+void pg_txn_free(pg_txn* txn);  /* abandon without commit                    */
+
+/* ---- ACL ingestion (vpp-agent key space) and introspection -------------------------- */
+int pg_apply_txn(pg_ctx* ctx, int resync, const pg_acl_op* ops, size_t n_ops);
+int pg_num_acls(pg_ctx* ctx);
+int pg_num_acl_changes(pg_ctx* ctx);
+int pg_num_committed_txns(pg_ctx* ctx);
+/* JSON of one ACL ({"name","ingress","egress","rules":[...]}) -> bytes needed (incl. NUL). */
+int pg_acl_json(pg_ctx* ctx, const char* acl_name, char* buf, size_t cap);
+/* JSON array of all installed ACL names (sorted) -> bytes needed (incl. NUL) */
+int pg_acl_names_json(pg_ctx* ctx, char* buf, size_t cap);
+/* names of the ACLs bound to an interface ("" when none) */
+int pg_interface_acls(pg_ctx* ctx, const char* if_name, char* inbound, size_t in_cap, char* outbound,
+                      size_t out_cap);
+
+/* ---- device tables and classification ---------------------------------------------- */
+int pg_sync_tables(pg_ctx* ctx); /* compile + upload (double-buffered swap); implicit in classify */
+int pg_table_id(pg_ctx* ctx, const char* acl_name);
+int pg_num_tables(pg_ctx* ctx);
+int pg_num_counter_slots(pg_ctx* ctx);
+/* global rule slot -> (table id, rule index in its ACL); rule index -1 for a table's
+ * default-deny slot; table id -1 for the "no ACL" (permit) slot */
+int pg_slot_info(pg_ctx* ctx, uint32_t slot, int32_t* table_id, int32_t* rule_index);
+
+int pg_classify(pg_ctx* ctx, int mode, int table_id, const pg_tuple_soa* tuples, uint64_t n, uint32_t* out,
+                uint64_t* counters, void* hip_stream);
+/* reference-shaped linear-scan kernel (K1) on one table, for validation and comparison */
+int pg_classify_linear(pg_ctx* ctx, int table_id, const pg_tuple_soa* tuples, uint64_t n, uint32_t* out,
+                       void* hip_stream);
+/* device-resident per-rule hit counters (u64, pg_num_counter_slots entries) */
+uint64_t* pg_counters_device(pg_ctx* ctx);
+int pg_reset_counters(pg_ctx* ctx, void* hip_stream);
+int pg_read_counters(pg_ctx* ctx, uint64_t* host_out, size_t n);
+
+/* ---- synthetic input generation on device (bench / parity workloads) ----------------- */
+typedef struct pg_gen_spec {
+    uint64_t seed;
+    uint64_t index_base;      /* global index of tuple 0 (multi-GPU shards)               */
+    int32_t table_id;         /* >= 0: "inside a rule" sampling from this table           */
+    uint32_t inside_pct;      /* % of tuples sampled inside a rule's predicate            */
+    const uint32_t* ip_pool;  /* host array: pool of "known" IPs (pods / internet hosts)  */
+    uint32_t n_ip_pool;
+    uint32_t pool_pct;        /* % of src/dst drawn from ip_pool (else uniform u32)       */
+    const uint16_t* port_pool;/* host array of popular dst ports                          */
+    uint32_t n_port_pool;
+    uint32_t port_pool_pct;   /* % of dst ports drawn from port_pool                      */
+    uint32_t tcp_pct, udp_pct;/* protocol mix (rest OTHER)                                */
+    const uint32_t* zipf_cdf; /* host array, n_rules+1 entries scaled to 2^32: rule index  *
+                               * follows it (config 4); NULL = uniform rule choice        */
+    uint32_t nomatch_pct;     /* % forced outside every rule's src (config 4)             */
+    uint32_t dst_pool_pct;    /* % of dst drawn from ip_pool (config 3/5: local pods)     */
+} pg_gen_spec;
+
+int pg_gen_tuples(pg_ctx* ctx, const pg_gen_spec* spec, uint64_t n, uint32_t* src_ip, uint32_t* dst_ip,
+                  uint16_t* src_port, uint16_t* dst_port, uint8_t* proto, void* hip_stream);
+
+/* ---- Connection* (MockACLEngine) evaluated on the device ------------------------------ */
+typedef struct pg_conn_query {
+    int32_t kind;              /* 0 PodToPod, 1 PodToInternet, 2 InternetToPod */
+    const char* src_namespace; /* pod endpoints                                  */
+    const char* src_name;
+    const char* dst_namespace;
+    const char* dst_name;
+    const char* src_ip;        /* internet endpoints (string, net.ParseIP)       */
+    const char* dst_ip;
+    int32_t protocol;
+    uint16_t src_port;
+    uint16_t dst_port;
+} pg_conn_query;
+/* out[i] = ConnAction; out_slot (optional) = deciding slot per query */
+int pg_connections(pg_ctx* ctx, const pg_conn_query* q, size_t n, int32_t* out, uint32_t* out_slot);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* POLICYGPU_H */

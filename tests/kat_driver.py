@@ -170,3 +170,78 @@ class OracleBackend:
 
     def acl_by_name(self, name):
         return self.acl_dict(self.engine.acl_by_name(name))
+
+
+# --- product backend (C ABI) ----------------------------------------------------
+class ProductBackend:
+    """Drives vpp_amd (C++ renderer + device engine). With ``gpu=False`` the Connection*
+    verdicts are not evaluated (they need the device); everything else runs on the host."""
+
+    def __init__(self, gpu=True):
+        import vpp_amd.renderer as R
+        self.R = R
+        self.gpu = gpu
+
+    def rule(self, d):
+        R = self.R
+        return R.ContivRule(ACTION[d["action"]], R.IPNet(d["src"]), R.IPNet(d["dst"]), PROTO[d["proto"]],
+                            d["sport"], d["dport"])
+
+    def setup(self, s):
+        R = self.R
+        self.engine = R.Engine(0)
+        e = self.engine
+        e.SetMainInterfaceName(s["main_if"])
+        e.SetVxlanBVIIfName(s["vxlan_bvi"])
+        e.SetHostInterconnectIfName(s["host_interconnect"])
+        e.SetOtherVPPInterfaces(s["other_ifs"])
+        for pod, ifn in s["pod_ifs"].items():
+            e.SetPodIfName(pod, ifn)
+        for pod, ip, another in s["pods"]:
+            e.RegisterPod(pod, ip, another)
+        self.restart()
+
+    def restart(self):
+        self.base_txns = self.engine.NumCommittedTxns()
+        self.renderer = self.R.Renderer(self.engine)
+
+    def txn(self, resync, renders):
+        t = self.renderer.NewTxn(resync)
+        for r in renders:
+            t.Render(r["pod"], self.R.IPNet.host(r["ip"]), [self.rule(x) for x in r["ingress"]],
+                     [self.rule(x) for x in r["egress"]], r["removed"])
+        return t.Commit()
+
+    def connections(self, checks):
+        if not self.gpu:
+            return [None] * len(checks)
+        qs = []
+        for c in checks:
+            a = c["args"]
+            kind = c["kind"].replace("Connection", "")
+            qs.append((kind, a[0], a[1], PROTO[a[2]], a[3], a[4]))
+        return self.engine.connections(qs)[0]
+
+    def num_acls(self):
+        return self.engine.GetNumOfACLs()
+
+    def num_acl_changes(self):
+        return self.engine.GetNumOfACLChanges()
+
+    def committed_txns(self):
+        return self.engine.NumCommittedTxns() - self.base_txns
+
+    @staticmethod
+    def acl_dict(acl):
+        if acl is None:
+            return None
+        return {"name": acl["name"], "ingress": acl["ingress"], "egress": acl["egress"],
+                "rules": [{"action": r["action"], "src": r["src"], "dst": r["dst"], "tcp": r["tcp"] is not None,
+                           "udp": r["udp"] is not None, "icmp": r["icmp"], "macip": r["macip"],
+                           "ip_rule": r["ip_rule"], "ip": r["ip"]} for r in acl["rules"]]}
+
+    def inbound_acl(self, ifn):
+        return self.acl_dict(self.engine.GetInboundACL(ifn))
+
+    def acl_by_name(self, name):
+        return self.acl_dict(self.engine.GetACLByName(name))

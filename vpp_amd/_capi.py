@@ -1,0 +1,125 @@
+"""ctypes binding of include/policygpu.h (the same C ABI a cgo stub would bind).
+
+The shared library is built in-tree (``vpp_amd/libpolicygpu.so``, see
+``__graft_entry__.build()``). There is no fallback: if the library is missing the import
+fails loudly, so nothing can silently run on the CPU.
+"""
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libpolicygpu.so")
+
+PG_OK, PG_ENOENT, PG_EIO, PG_ENOMEM, PG_EINVAL, PG_EFAULT = 0, -2, -5, -12, -22, -14
+MODE_SINGLE, MODE_PERPOD, MODE_CONN = 0, 1, 2
+ORIENT_INGRESS, ORIENT_EGRESS = 0, 1
+
+
+class pg_ipnet(C.Structure):
+    _fields_ = [("family", C.c_uint8), ("prefix_len", C.c_uint8), ("_pad", C.c_uint8 * 2), ("addr", C.c_uint8 * 16)]
+
+
+class pg_contiv_rule(C.Structure):
+    _fields_ = [("action", C.c_int32), ("protocol", C.c_int32), ("src_port", C.c_uint16), ("dst_port", C.c_uint16),
+                ("src", pg_ipnet), ("dst", pg_ipnet)]
+
+
+class pg_port_range(C.Structure):
+    _fields_ = [("lower_port", C.c_uint32), ("upper_port", C.c_uint32)]
+
+
+class pg_l4(C.Structure):
+    _fields_ = [("present", C.c_uint8), ("has_src_range", C.c_uint8), ("has_dst_range", C.c_uint8),
+                ("_pad", C.c_uint8), ("src_range", pg_port_range), ("dst_range", pg_port_range)]
+
+
+class pg_acl_rule(C.Structure):
+    _fields_ = [("action", C.c_int32), ("has_macip_rule", C.c_uint8), ("has_ip_rule", C.c_uint8),
+                ("has_ip", C.c_uint8), ("has_icmp", C.c_uint8), ("src_network", C.c_char_p),
+                ("dst_network", C.c_char_p), ("tcp", pg_l4), ("udp", pg_l4)]
+
+
+class pg_acl(C.Structure):
+    _fields_ = [("name", C.c_char_p), ("rules", C.POINTER(pg_acl_rule)), ("n_rules", C.c_size_t),
+                ("ingress", C.POINTER(C.c_char_p)), ("n_ingress", C.c_size_t),
+                ("egress", C.POINTER(C.c_char_p)), ("n_egress", C.c_size_t)]
+
+
+class pg_acl_op(C.Structure):
+    _fields_ = [("key", C.c_char_p), ("value", C.POINTER(pg_acl))]
+
+
+class pg_tuple_soa(C.Structure):
+    _fields_ = [("src_ip", C.c_void_p), ("dst_ip", C.c_void_p), ("src_port", C.c_void_p),
+                ("dst_port", C.c_void_p), ("proto", C.c_void_p)]
+
+
+class pg_gen_spec(C.Structure):
+    _fields_ = [("seed", C.c_uint64), ("index_base", C.c_uint64), ("table_id", C.c_int32),
+                ("inside_pct", C.c_uint32), ("ip_pool", C.POINTER(C.c_uint32)), ("n_ip_pool", C.c_uint32),
+                ("pool_pct", C.c_uint32), ("port_pool", C.POINTER(C.c_uint16)), ("n_port_pool", C.c_uint32),
+                ("port_pool_pct", C.c_uint32), ("tcp_pct", C.c_uint32), ("udp_pct", C.c_uint32),
+                ("zipf_cdf", C.POINTER(C.c_uint32)), ("nomatch_pct", C.c_uint32), ("dst_pool_pct", C.c_uint32)]
+
+
+class pg_conn_query(C.Structure):
+    _fields_ = [("kind", C.c_int32), ("src_namespace", C.c_char_p), ("src_name", C.c_char_p),
+                ("dst_namespace", C.c_char_p), ("dst_name", C.c_char_p), ("src_ip", C.c_char_p),
+                ("dst_ip", C.c_char_p), ("protocol", C.c_int32), ("src_port", C.c_uint16), ("dst_port", C.c_uint16)]
+
+
+_P = C.c_void_p
+_SIGS = {
+    "pg_version": (C.c_char_p, []),
+    "pg_create": (_P, [C.c_int]),
+    "pg_destroy": (None, [_P]),
+    "pg_last_error": (C.c_char_p, [_P]),
+    "pg_set_pod_if_name": (C.c_int, [_P, C.c_char_p, C.c_char_p, C.c_char_p]),
+    "pg_set_host_interconnect_if_name": (C.c_int, [_P, C.c_char_p]),
+    "pg_set_main_interface_name": (C.c_int, [_P, C.c_char_p]),
+    "pg_set_other_vpp_interfaces": (C.c_int, [_P, C.POINTER(C.c_char_p), C.c_size_t]),
+    "pg_set_vxlan_bvi_if_name": (C.c_int, [_P, C.c_char_p]),
+    "pg_register_pod": (C.c_int, [_P, C.c_char_p, C.c_char_p, C.c_char_p, C.c_int]),
+    "pg_renderer_new": (_P, [_P, C.c_int]),
+    "pg_renderer_free": (None, [_P]),
+    "pg_renderer_new_txn": (_P, [_P, C.c_int]),
+    "pg_txn_render": (C.c_int, [_P, C.c_char_p, C.c_char_p, C.POINTER(pg_ipnet), C.POINTER(pg_contiv_rule),
+                                C.c_size_t, C.POINTER(pg_contiv_rule), C.c_size_t, C.c_int]),
+    "pg_txn_commit": (C.c_int, [_P]),
+    "pg_txn_free": (None, [_P]),
+    "pg_apply_txn": (C.c_int, [_P, C.c_int, C.POINTER(pg_acl_op), C.c_size_t]),
+    "pg_num_acls": (C.c_int, [_P]),
+    "pg_num_acl_changes": (C.c_int, [_P]),
+    "pg_num_committed_txns": (C.c_int, [_P]),
+    "pg_acl_json": (C.c_int, [_P, C.c_char_p, C.c_char_p, C.c_size_t]),
+    "pg_acl_names_json": (C.c_int, [_P, C.c_char_p, C.c_size_t]),
+    "pg_interface_acls": (C.c_int, [_P, C.c_char_p, C.c_char_p, C.c_size_t, C.c_char_p, C.c_size_t]),
+    "pg_sync_tables": (C.c_int, [_P]),
+    "pg_table_id": (C.c_int, [_P, C.c_char_p]),
+    "pg_num_tables": (C.c_int, [_P]),
+    "pg_num_counter_slots": (C.c_int, [_P]),
+    "pg_slot_info": (C.c_int, [_P, C.c_uint32, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
+    "pg_classify": (C.c_int, [_P, C.c_int, C.c_int, C.POINTER(pg_tuple_soa), C.c_uint64, _P, _P, _P]),
+    "pg_classify_linear": (C.c_int, [_P, C.c_int, C.POINTER(pg_tuple_soa), C.c_uint64, _P, _P]),
+    "pg_counters_device": (_P, [_P]),
+    "pg_reset_counters": (C.c_int, [_P, _P]),
+    "pg_read_counters": (C.c_int, [_P, C.POINTER(C.c_uint64), C.c_size_t]),
+    "pg_gen_tuples": (C.c_int, [_P, C.POINTER(pg_gen_spec), C.c_uint64, _P, _P, _P, _P, _P, _P]),
+    "pg_connections": (C.c_int, [_P, C.POINTER(pg_conn_query), C.c_size_t, C.POINTER(C.c_int32),
+                                 C.POINTER(C.c_uint32)]),
+}
+EXPORTED = sorted(_SIGS)
+
+
+def load(path=LIB_PATH):
+    if not os.path.exists(path):
+        raise ImportError("libpolicygpu.so not built (%s): run __graft_entry__.build()" % path)
+    lib = C.CDLL(path)
+    for name, (res, args) in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+lib = load()

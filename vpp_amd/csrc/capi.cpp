@@ -1,0 +1,551 @@
+// extern "C" boundary (include/policygpu.h). Converts the flat C structs into the host
+// model, forwards to the renderer / engine and maps failures to PG_* codes + last_error.
+#include <cstring>
+#include <memory>
+#include <stdexcept>
+
+#include "../../include/policygpu.h"
+#include "engine.hpp"
+
+using namespace pg;
+
+struct pg_ctx {
+    Engine eng;
+};
+struct pg_renderer {
+    pg_ctx* ctx;
+    std::unique_ptr<Renderer> r;
+};
+struct pg_txn {
+    pg_ctx* ctx;
+    std::unique_ptr<RendererTxn> t;
+};
+
+namespace {
+
+IPNet to_ipnet(const pg_ipnet& n) {
+    IPNet r;
+    if (n.family == 4) {
+        r.ip = mk(n.addr, 4);
+        r.mask = cidr_mask(n.prefix_len, 32);
+    } else if (n.family == 6) {
+        r.ip = mk(n.addr, 16);
+        r.mask = cidr_mask(n.prefix_len, 128);
+    }
+    return r;
+}
+
+ContivRule to_rule(const pg_contiv_rule& c) {
+    ContivRule r;
+    r.action = c.action;
+    r.protocol = c.protocol;
+    r.src_port = c.src_port;
+    r.dst_port = c.dst_port;
+    r.src = to_ipnet(c.src);
+    r.dst = to_ipnet(c.dst);
+    return r;
+}
+
+std::string sv(const char* s) { return s ? std::string(s) : std::string(); }
+
+L4Section to_l4(const pg_l4& l) {
+    L4Section s;
+    s.present = l.present;
+    s.has_src = l.has_src_range;
+    s.has_dst = l.has_dst_range;
+    s.src = {l.src_range.lower_port, l.src_range.upper_port};
+    s.dst = {l.dst_range.lower_port, l.dst_range.upper_port};
+    return s;
+}
+
+ACLPtr to_acl(const pg_acl& a) {
+    auto acl = std::make_shared<ACL>();
+    acl->name = sv(a.name);
+    for (size_t i = 0; i < a.n_rules; i++) {
+        const pg_acl_rule& x = a.rules[i];
+        AclRule r;
+        r.action = x.action;
+        r.has_macip = x.has_macip_rule;
+        r.has_ip_rule = x.has_ip_rule;
+        r.has_ip = x.has_ip;
+        r.has_icmp = x.has_icmp;
+        r.src_network = sv(x.src_network);
+        r.dst_network = sv(x.dst_network);
+        r.tcp = to_l4(x.tcp);
+        r.udp = to_l4(x.udp);
+        acl->rules.push_back(r);
+    }
+    for (size_t i = 0; i < a.n_ingress; i++) acl->ingress.push_back(sv(a.ingress[i]));
+    for (size_t i = 0; i < a.n_egress; i++) acl->egress.push_back(sv(a.egress[i]));
+    return acl;
+}
+
+int fail(pg_ctx* c, int code, const std::string& msg) {
+    if (c) c->eng.last_error = msg;
+    return code;
+}
+
+std::string json_escape(const std::string& s) {
+    std::string o;
+    for (char ch : s) {
+        if (ch == '"' || ch == '\\') o += '\\';
+        o += ch;
+    }
+    return o;
+}
+
+uint32_t pkt_key_host(int proto, uint16_t port) {
+    switch (proto) {
+        case kTCP: return port;
+        case kUDP: return kKeyUDP | port;
+        case kOTHER: return kKeyOTHER;
+    }
+    return kKeyANY;
+}
+
+}  // namespace
+
+#define GUARD_BEGIN try {
+#define GUARD_END(ctx)                                         \
+    }                                                          \
+    catch (const std::exception& e) {                          \
+        return fail(ctx, PG_EFAULT, e.what());                 \
+    }                                                          \
+    catch (...) {                                              \
+        return fail(ctx, PG_EFAULT, "unknown C++ exception");  \
+    }
+
+extern "C" {
+
+const char* pg_version(void) { return "policygpu 0.1 (gfx950)"; }
+
+pg_ctx* pg_create(int hip_device) {
+    auto* c = new (std::nothrow) pg_ctx();
+    if (!c) return nullptr;
+    c->eng.device = hip_device;
+    std::string err;
+    if (dev_set_device(hip_device, &err) != 0) c->eng.last_error = err;
+    return c;
+}
+
+void pg_destroy(pg_ctx* ctx) { delete ctx; }
+
+const char* pg_last_error(const pg_ctx* ctx) { return ctx ? ctx->eng.last_error.c_str() : "null context"; }
+
+int pg_set_pod_if_name(pg_ctx* ctx, const char* ns, const char* name, const char* if_name) {
+    if (!ctx || !ns || !name || !if_name) return PG_EINVAL;
+    ctx->eng.ifaces.pod_if[PodID{ns, name}] = if_name;
+    ctx->eng.dirty = true;
+    return PG_OK;
+}
+int pg_set_host_interconnect_if_name(pg_ctx* ctx, const char* n) {
+    if (!ctx) return PG_EINVAL;
+    ctx->eng.ifaces.host_interconnect = sv(n);
+    ctx->eng.dirty = true;
+    return PG_OK;
+}
+int pg_set_main_interface_name(pg_ctx* ctx, const char* n) {
+    if (!ctx) return PG_EINVAL;
+    ctx->eng.ifaces.main_if = sv(n);
+    ctx->eng.dirty = true;
+    return PG_OK;
+}
+int pg_set_other_vpp_interfaces(pg_ctx* ctx, const char* const* names, size_t n) {
+    if (!ctx) return PG_EINVAL;
+    ctx->eng.ifaces.other_ifs.clear();
+    for (size_t i = 0; i < n; i++) ctx->eng.ifaces.other_ifs.push_back(sv(names[i]));
+    ctx->eng.dirty = true;
+    return PG_OK;
+}
+int pg_set_vxlan_bvi_if_name(pg_ctx* ctx, const char* n) {
+    if (!ctx) return PG_EINVAL;
+    ctx->eng.ifaces.vxlan_bvi = sv(n);
+    ctx->eng.dirty = true;
+    return PG_OK;
+}
+int pg_register_pod(pg_ctx* ctx, const char* ns, const char* name, const char* ip, int another_node) {
+    if (!ctx || !ns || !name || !ip) return PG_EINVAL;
+    PodReg reg;
+    parse_ip(ip, &reg.ip);  // net.ParseIP; nil on failure like the reference
+    reg.another_node = another_node != 0;
+    ctx->eng.pods[PodID{ns, name}] = reg;
+    ctx->eng.dirty = true;
+    return PG_OK;
+}
+
+pg_renderer* pg_renderer_new(pg_ctx* ctx, int orientation) {
+    if (!ctx) return nullptr;
+    auto* r = new (std::nothrow) pg_renderer();
+    if (!r) return nullptr;
+    r->ctx = ctx;
+    r->r.reset(new Renderer(&ctx->eng.ifaces, &ctx->eng, engine_apply_cb,
+                            orientation == PG_ORIENT_INGRESS ? kIngressOrientation : kEgressOrientation));
+    return r;
+}
+void pg_renderer_free(pg_renderer* r) { delete r; }
+
+pg_txn* pg_renderer_new_txn(pg_renderer* r, int resync) {
+    if (!r) return nullptr;
+    auto* t = new (std::nothrow) pg_txn();
+    if (!t) return nullptr;
+    t->ctx = r->ctx;
+    t->t.reset(new RendererTxn(r->r.get(), resync != 0));
+    return t;
+}
+
+int pg_txn_render(pg_txn* txn, const char* ns, const char* name, const pg_ipnet* pod_ip,
+                  const pg_contiv_rule* ingress, size_t n_in, const pg_contiv_rule* egress, size_t n_eg, int removed) {
+    if (!txn || !ns || !name) return PG_EINVAL;
+    GUARD_BEGIN
+    std::vector<ContivRule> in, eg;
+    for (size_t i = 0; i < n_in; i++) in.push_back(to_rule(ingress[i]));
+    for (size_t i = 0; i < n_eg; i++) eg.push_back(to_rule(egress[i]));
+    IPNet ip;
+    const IPNet* pip = nullptr;
+    if (pod_ip && pod_ip->family != 0) {
+        ip = to_ipnet(*pod_ip);
+        pip = &ip;
+    }
+    txn->t->render(PodID{ns, name}, pip, std::move(in), std::move(eg), removed != 0);
+    return PG_OK;
+    GUARD_END(txn->ctx)
+}
+
+int pg_txn_commit(pg_txn* txn) {
+    if (!txn) return PG_EINVAL;
+    pg_ctx* ctx = txn->ctx;
+    int rc = PG_OK;
+    try {
+        std::string e = txn->t->commit();
+        if (!e.empty()) rc = fail(ctx, PG_EFAULT, e);
+    } catch (const std::exception& ex) {
+        rc = fail(ctx, PG_EFAULT, ex.what());
+    }
+    delete txn;
+    return rc;
+}
+void pg_txn_free(pg_txn* txn) { delete txn; }
+
+int pg_apply_txn(pg_ctx* ctx, int resync, const pg_acl_op* ops, size_t n) {
+    if (!ctx) return PG_EINVAL;
+    GUARD_BEGIN
+    static const std::string prefix = "config/vpp/acls/v2/acl/";
+    AclOps m;
+    for (size_t i = 0; i < n; i++) {
+        std::string key = sv(ops[i].key);
+        if (key.compare(0, prefix.size(), prefix) != 0) return fail(ctx, PG_EFAULT, "non-ACL changed in txn");
+        std::string name = key.substr(prefix.size());
+        if (ops[i].value) {
+            m[name] = to_acl(*ops[i].value);
+        } else {
+            if (resync) return fail(ctx, PG_EFAULT, "failed to cast ACL value");
+            m[name] = nullptr;
+        }
+    }
+    std::string e = ctx->eng.apply_txn(resync != 0, m);
+    if (!e.empty()) return fail(ctx, PG_EFAULT, e);
+    return PG_OK;
+    GUARD_END(ctx)
+}
+
+int pg_num_acls(pg_ctx* ctx) { return ctx ? (int)ctx->eng.by_name.size() : PG_EINVAL; }
+int pg_num_acl_changes(pg_ctx* ctx) { return ctx ? ctx->eng.changes : PG_EINVAL; }
+int pg_num_committed_txns(pg_ctx* ctx) { return ctx ? ctx->eng.committed : PG_EINVAL; }
+
+int pg_acl_json(pg_ctx* ctx, const char* acl_name, char* buf, size_t cap) {
+    if (!ctx || !acl_name) return PG_EINVAL;
+    auto it = ctx->eng.by_name.find(acl_name);
+    if (it == ctx->eng.by_name.end()) return PG_ENOENT;
+    const ACL& a = *it->second;
+    std::string s = "{\"name\":\"" + json_escape(a.name) + "\",\"ingress\":[";
+    for (size_t i = 0; i < a.ingress.size(); i++) s += (i ? ",\"" : "\"") + json_escape(a.ingress[i]) + "\"";
+    s += "],\"egress\":[";
+    for (size_t i = 0; i < a.egress.size(); i++) s += (i ? ",\"" : "\"") + json_escape(a.egress[i]) + "\"";
+    s += "],\"rules\":[";
+    auto l4 = [](const L4Section& x) {
+        if (!x.present) return std::string("null");
+        return "{\"src\":[" + std::to_string(x.src.lower) + "," + std::to_string(x.src.upper) + "],\"dst\":[" +
+               std::to_string(x.dst.lower) + "," + std::to_string(x.dst.upper) + "]}";
+    };
+    for (size_t i = 0; i < a.rules.size(); i++) {
+        const AclRule& r = a.rules[i];
+        if (i) s += ",";
+        s += "{\"action\":" + std::to_string(r.action) + ",\"src\":\"" + json_escape(r.src_network) +
+             "\",\"dst\":\"" + json_escape(r.dst_network) + "\",\"tcp\":" + l4(r.tcp) + ",\"udp\":" + l4(r.udp) +
+             ",\"icmp\":" + (r.has_icmp ? "true" : "false") + ",\"macip\":" + (r.has_macip ? "true" : "false") +
+             ",\"ip_rule\":" + (r.has_ip_rule ? "true" : "false") + ",\"ip\":" + (r.has_ip ? "true" : "false") + "}";
+    }
+    s += "]}";
+    if (buf && cap > 0) {
+        size_t k = std::min(cap - 1, s.size());
+        std::memcpy(buf, s.data(), k);
+        buf[k] = 0;
+    }
+    return (int)s.size() + 1;
+}
+
+int pg_acl_names_json(pg_ctx* ctx, char* buf, size_t cap) {
+    if (!ctx) return PG_EINVAL;
+    std::string s = "[";
+    bool first = true;
+    for (auto& kv : ctx->eng.by_name) {
+        s += (first ? "\"" : ",\"") + json_escape(kv.first) + "\"";
+        first = false;
+    }
+    s += "]";
+    if (buf && cap > 0) {
+        size_t k = std::min(cap - 1, s.size());
+        std::memcpy(buf, s.data(), k);
+        buf[k] = 0;
+    }
+    return (int)s.size() + 1;
+}
+
+int pg_interface_acls(pg_ctx* ctx, const char* if_name, char* inbound, size_t in_cap, char* outbound,
+                      size_t out_cap) {
+    if (!ctx || !if_name) return PG_EINVAL;
+    std::string in, out;
+    auto it = ctx->eng.by_if.find(if_name);
+    if (it != ctx->eng.by_if.end()) {
+        if (it->second.first) in = it->second.first->name;
+        if (it->second.second) out = it->second.second->name;
+    }
+    auto cp = [](char* b, size_t cap, const std::string& s) {
+        if (b && cap) {
+            size_t k = std::min(cap - 1, s.size());
+            std::memcpy(b, s.data(), k);
+            b[k] = 0;
+        }
+    };
+    cp(inbound, in_cap, in);
+    cp(outbound, out_cap, out);
+    return PG_OK;
+}
+
+int pg_sync_tables(pg_ctx* ctx) {
+    if (!ctx) return PG_EINVAL;
+    GUARD_BEGIN
+    return ctx->eng.sync();
+    GUARD_END(ctx)
+}
+
+int pg_table_id(pg_ctx* ctx, const char* acl_name) {
+    if (!ctx || !acl_name) return PG_EINVAL;
+    int rc = pg_sync_tables(ctx);
+    if (rc) return rc;
+    auto it = ctx->eng.table_of_acl.find(acl_name);
+    return it == ctx->eng.table_of_acl.end() ? PG_ENOENT : it->second;
+}
+
+int pg_num_tables(pg_ctx* ctx) {
+    if (!ctx) return PG_EINVAL;
+    int rc = pg_sync_tables(ctx);
+    return rc ? rc : (int)ctx->eng.table_names.size();
+}
+
+int pg_num_counter_slots(pg_ctx* ctx) {
+    if (!ctx) return PG_EINVAL;
+    int rc = pg_sync_tables(ctx);
+    return rc ? rc : (int)ctx->eng.counter_slots;
+}
+
+int pg_slot_info(pg_ctx* ctx, uint32_t slot, int32_t* table_id, int32_t* rule_index) {
+    if (!ctx) return PG_EINVAL;
+    int rc = pg_sync_tables(ctx);
+    if (rc) return rc;
+    if (slot >= ctx->eng.slot_table.size()) return PG_EINVAL;
+    if (table_id) *table_id = ctx->eng.slot_table[slot];
+    if (rule_index) *rule_index = ctx->eng.slot_rule[slot];
+    return PG_OK;
+}
+
+int pg_classify(pg_ctx* ctx, int mode, int table_id, const pg_tuple_soa* t, uint64_t n, uint32_t* out,
+                uint64_t* counters, void* stream) {
+    if (!ctx || !t || !out || mode < 0 || mode > 2) return PG_EINVAL;
+    GUARD_BEGIN
+    int rc = ctx->eng.sync();
+    if (rc) return rc;
+    const DevTableSet& T = *ctx->eng.view();
+    if (mode == PG_MODE_SINGLE && (table_id < 0 || (uint32_t)table_id >= T.n_tables))
+        return fail(ctx, PG_EINVAL, "table id out of range");
+    if (!t->src_ip || !t->dst_ip || !t->dst_port || !t->proto || (mode == PG_MODE_CONN && !t->src_port))
+        return fail(ctx, PG_EINVAL, "missing tuple field");
+    std::string err;
+    if (dev_classify(T, mode, table_id, t->src_ip, t->dst_ip, t->src_port, t->dst_port, t->proto, n, out,
+                     (unsigned long long*)counters, stream, &err) != 0)
+        return fail(ctx, PG_EIO, err);
+    return PG_OK;
+    GUARD_END(ctx)
+}
+
+int pg_classify_linear(pg_ctx* ctx, int table_id, const pg_tuple_soa* t, uint64_t n, uint32_t* out, void* stream) {
+    if (!ctx || !t || !out) return PG_EINVAL;
+    GUARD_BEGIN
+    int rc = ctx->eng.sync();
+    if (rc) return rc;
+    const DevTableSet& T = *ctx->eng.view();
+    if (table_id < 0 || (uint32_t)table_id >= T.n_tables) return fail(ctx, PG_EINVAL, "table id out of range");
+    std::string err;
+    if (dev_classify_linear(T, table_id, t->src_ip, t->dst_ip, t->dst_port, t->proto, n, out, stream, &err) != 0)
+        return fail(ctx, PG_EIO, err);
+    return PG_OK;
+    GUARD_END(ctx)
+}
+
+uint64_t* pg_counters_device(pg_ctx* ctx) {
+    if (!ctx || ctx->eng.sync() != PG_OK) return nullptr;
+    return (uint64_t*)ctx->eng.counters;
+}
+
+int pg_reset_counters(pg_ctx* ctx, void* stream) {
+    if (!ctx) return PG_EINVAL;
+    int rc = ctx->eng.sync();
+    if (rc) return rc;
+    std::string err;
+    if (dev_memset(ctx->eng.counters, 0, ctx->eng.counter_slots * 8, stream, &err) != 0)
+        return fail(ctx, PG_EIO, err);
+    return PG_OK;
+}
+
+int pg_read_counters(pg_ctx* ctx, uint64_t* host_out, size_t n) {
+    if (!ctx || !host_out) return PG_EINVAL;
+    int rc = ctx->eng.sync();
+    if (rc) return rc;
+    size_t k = std::min(n, ctx->eng.counter_slots);
+    std::string err;
+    if (dev_sync(&err) != 0 || dev_copy_d2h(host_out, ctx->eng.counters, k * 8, &err) != 0)
+        return fail(ctx, PG_EIO, err);
+    return (int)k;
+}
+
+int pg_gen_tuples(pg_ctx* ctx, const pg_gen_spec* spec, uint64_t n, uint32_t* src, uint32_t* dst, uint16_t* sport,
+                  uint16_t* dport, uint8_t* proto, void* stream) {
+    if (!ctx || !spec || !src || !dst || !dport || !proto) return PG_EINVAL;
+    GUARD_BEGIN
+    int rc = ctx->eng.sync();
+    if (rc) return rc;
+    const DevTableSet& T = *ctx->eng.view();
+    if (spec->table_id >= 0 && (uint32_t)spec->table_id >= T.n_tables) return fail(ctx, PG_EINVAL, "table id");
+    if (spec->table_id >= 0 && spec->inside_pct > 0) {
+        std::vector<DevTable> tabs(1);
+        // n_rules of the table must be > 0 for inside sampling
+        auto it = ctx->eng.by_name.find(ctx->eng.table_names[spec->table_id]);
+        if (it->second->rules.empty()) return fail(ctx, PG_EINVAL, "inside sampling on an empty table");
+    }
+    std::string err;
+    GenParams g{};
+    g.seed = spec->seed;
+    g.index_base = spec->index_base;
+    g.table_id = spec->table_id;
+    g.inside_pct = spec->inside_pct;
+    g.pool_pct = spec->pool_pct;
+    g.port_pool_pct = spec->port_pool_pct;
+    g.tcp_pct = spec->tcp_pct;
+    g.udp_pct = spec->udp_pct;
+    g.nomatch_pct = spec->nomatch_pct;
+    g.dst_pool_pct = spec->dst_pool_pct;
+    g.n_ip_pool = spec->ip_pool ? spec->n_ip_pool : 0;
+    g.n_port_pool = spec->port_pool ? spec->n_port_pool : 0;
+    void *ipp = nullptr, *pp = nullptr, *zc = nullptr;
+    auto cleanup = [&]() {
+        dev_sync(nullptr);
+        dev_release(ipp);
+        dev_release(pp);
+        dev_release(zc);
+    };
+    if (g.n_ip_pool) {
+        ipp = dev_alloc(g.n_ip_pool * 4, &err);
+        if (!ipp || dev_copy_h2d(ipp, spec->ip_pool, g.n_ip_pool * 4, &err)) return cleanup(), fail(ctx, PG_EIO, err);
+        g.ip_pool = (const uint32_t*)ipp;
+    }
+    if (g.n_port_pool) {
+        pp = dev_alloc(g.n_port_pool * 2, &err);
+        if (!pp || dev_copy_h2d(pp, spec->port_pool, g.n_port_pool * 2, &err)) return cleanup(), fail(ctx, PG_EIO, err);
+        g.port_pool = (const uint16_t*)pp;
+    }
+    if (spec->zipf_cdf && spec->table_id >= 0) {
+        size_t nr = ctx->eng.by_name[ctx->eng.table_names[spec->table_id]]->rules.size();
+        zc = dev_alloc(nr * 4, &err);
+        if (!zc || dev_copy_h2d(zc, spec->zipf_cdf, nr * 4, &err)) return cleanup(), fail(ctx, PG_EIO, err);
+        g.zipf_cdf = (const uint32_t*)zc;
+    }
+    int r2 = dev_gen(T, g, n, src, dst, sport, dport, proto, stream, &err);
+    cleanup();
+    if (r2 != 0) return fail(ctx, PG_EIO, err);
+    return PG_OK;
+    GUARD_END(ctx)
+}
+
+// Connection* preamble (aclengine_mock.go:273-420) on the host, testConnection on the device.
+int pg_connections(pg_ctx* ctx, const pg_conn_query* q, size_t n, int32_t* out, uint32_t* out_slot) {
+    if (!ctx || (!q && n) || (!out && n)) return PG_EINVAL;
+    GUARD_BEGIN
+    Engine& E = ctx->eng;
+    int rc = E.sync();
+    if (rc) return rc;
+    const DevTableSet& T = *E.view();
+    std::vector<ConnQueryDev> dq;
+    std::vector<int64_t> where(n, -1);
+    std::string node_if = E.node_if_name();
+    for (size_t i = 0; i < n; i++) {
+        const pg_conn_query& c = q[i];
+        std::string sif, dif;
+        Bytes sip, dip;
+        bool ok = true;
+        auto pod_if = [&](const char* ns, const char* nm, bool allow_remote, std::string* ifn, Bytes* ip) {
+            auto it = E.pods.find(PodID{sv(ns), sv(nm)});
+            if (it == E.pods.end()) return false;
+            *ip = it->second.ip;
+            if (it->second.another_node) {
+                if (!allow_remote || node_if.empty()) return false;
+                *ifn = node_if;
+                return true;
+            }
+            return E.ifaces.if_name(PodID{sv(ns), sv(nm)}, ifn);
+        };
+        if (c.kind == 0) {
+            ok = pod_if(c.src_namespace, c.src_name, true, &sif, &sip) &&
+                 pod_if(c.dst_namespace, c.dst_name, true, &dif, &dip);
+        } else if (c.kind == 1) {
+            ok = pod_if(c.src_namespace, c.src_name, false, &sif, &sip) && !node_if.empty() &&
+                 parse_ip(sv(c.dst_ip), &dip);
+            dif = node_if;
+        } else if (c.kind == 2) {
+            ok = !node_if.empty() && parse_ip(sv(c.src_ip), &sip) &&
+                 pod_if(c.dst_namespace, c.dst_name, false, &dif, &dip);
+            sif = node_if;
+        } else {
+            return fail(ctx, PG_EINVAL, "bad query kind");
+        }
+        if (!ok) {
+            out[i] = PG_CONN_FAILURE;
+            if (out_slot) out_slot[i] = T.slot_unresolved;
+            continue;
+        }
+        Bytes s4, d4;
+        if (!to4(sip, &s4) || !to4(dip, &d4)) return fail(ctx, PG_EINVAL, "IPv6 endpoints are not classified");
+        ConnQueryDev d{};
+        d.src_ip = ipv4_u32(s4);
+        d.dst_ip = ipv4_u32(d4);
+        d.src_if = E.iface_of(sif);
+        d.dst_if = E.iface_of(dif);
+        if (d.src_if < 0 || d.dst_if < 0) return fail(ctx, PG_EFAULT, "interface not compiled");
+        d.key_syn = pkt_key_host(c.protocol, c.dst_port);
+        d.key_synack = pkt_key_host(c.protocol, c.src_port);
+        where[i] = (int64_t)dq.size();
+        dq.push_back(d);
+    }
+    std::vector<uint32_t> res(dq.size());
+    std::string err;
+    if (dev_conn_queries(T, dq.data(), dq.size(), res.data(), &err) != 0) return fail(ctx, PG_EIO, err);
+    for (size_t i = 0; i < n; i++) {
+        if (where[i] < 0) continue;
+        uint32_t w = res[where[i]];
+        out[i] = (int32_t)(w >> 30);
+        if (out_slot) out_slot[i] = w & 0x3FFFFFFFu;
+    }
+    return PG_OK;
+    GUARD_END(ctx)
+}
+
+}  // extern "C"

@@ -1,0 +1,119 @@
+// Device-side data layout shared by the host compiler (engine.cpp) and the HIP kernels
+// (device.hip). Everything here is plain-old-data copied to HBM as flat arrays.
+//
+// Layout in HBM (one "table set", double-buffered by the engine):
+//   rules    DevRule[NR]        all ACLs' rules, concatenated, ACL order preserved
+//   tabs     DevTable[T]        per-ACL header
+//   bnd      u32[]              per table: sorted start addresses of its src intervals
+//   ivl      uint2[]            per interval: {first candidate, candidate count}
+//   radix    u32[]              per table: 2^bits+1 entries, interval of (x << (32-bits))
+//   cand     uint4[]            per interval candidate list: {dnet, dmask, klo|act<<24, khi}
+//   cand_rule u32[]             rule index (in its ACL) of each candidate
+//   ifaces   int2[NI]           per interface {inbound table, outbound table} (-1 = no ACL)
+//   iphash   uint2[cap]         IPv4 -> interface (open addressing, EMPTY = 0xFFFFFFFF value)
+#pragma once
+#include <cstdint>
+#include <string>
+#include <vector>
+
+namespace pg {
+
+// Packet L4 key: TCP -> dport, UDP -> 0x10000|dport, OTHER -> 0x20000, else (ANY/invalid) 0x30000.
+constexpr uint32_t kKeyUDP = 0x10000u, kKeyOTHER = 0x20000u, kKeyANY = 0x30000u, kKeyMax = 0x2FFFFu;
+// ACLAction codes (aclengine_mock.go:56-71)
+constexpr uint32_t kActDeny = 0, kActPermit = 1, kActReflect = 2, kActFailure = 3, kActNever = 0xF;
+
+struct DevRule {           // 32 B, one compiled vpp_acl rule
+    uint32_t snet, smask;  // src: (src & smask) == snet
+    uint32_t dnet, dmask;  // dst
+    uint32_t klo, khi;     // L4 key range (empty when klo > khi)
+    uint32_t act;          // low nibble: action on key match; high nibble: action for ANY packets (F = never)
+    uint32_t pad;
+};
+
+struct DevTable {          // 32 B
+    uint32_t rule_base;    // first rule (global index == counter slot)
+    uint32_t n_rules;
+    uint32_t bnd_base;     // first interval (into bnd / ivl)
+    uint32_t nb;           // intervals (>= 1)
+    uint32_t radix_base;
+    uint32_t radix_shift;  // 32 - bits
+    uint32_t flags;
+    uint32_t pad;
+};
+
+struct DevTableSet {       // device pointers (valid on the GPU)
+    const DevRule* rules;
+    const DevTable* tabs;
+    const uint32_t* bnd;
+    const uint32_t* ivl;   // uint2 pairs
+    const uint32_t* radix;
+    const uint32_t* cand;  // uint4 quads
+    const uint32_t* cand_rule;
+    const int32_t* ifaces; // int2 pairs
+    const uint32_t* iphash;// uint2 pairs {ip, iface}
+    uint32_t iphash_mask;
+    int32_t node_if;       // interface of non-local IPs, -1 = none (FAILURE)
+    uint32_t n_rules;      // NR
+    uint32_t n_tables;     // T
+    uint32_t n_ifaces;
+    uint32_t slot_noacl;   // NR + T
+    uint32_t slot_unresolved;
+    uint32_t n_slots;
+};
+
+// Host image of a table set, produced by the compiler and uploaded as one blob.
+struct HostTableSet {
+    std::vector<DevRule> rules;
+    std::vector<DevTable> tabs;
+    std::vector<uint32_t> bnd, ivl, radix, cand, cand_rule;
+    std::vector<int32_t> ifaces;
+    std::vector<uint32_t> iphash;
+    uint32_t iphash_mask = 0;
+    int32_t node_if = -1;
+};
+
+struct GenParams {         // device view of pg_gen_spec
+    uint64_t seed, index_base;
+    int32_t table_id;
+    uint32_t inside_pct, pool_pct, port_pool_pct, tcp_pct, udp_pct, nomatch_pct, dst_pool_pct;
+    uint32_t n_ip_pool, n_port_pool;
+    const uint32_t* ip_pool;
+    const uint16_t* port_pool;
+    const uint32_t* zipf_cdf;  // n_rules+1 entries or null
+};
+
+struct ConnQueryDev {      // resolved Connection* query
+    uint32_t src_ip, dst_ip;
+    int32_t src_if, dst_if;
+    uint32_t key_syn;      // L4 key with dport
+    uint32_t key_synack;   // L4 key with sport
+    uint32_t same_if;
+    uint32_t pad;
+};
+
+// ---- device API (device.hip) ----------------------------------------------------------
+struct DeviceBuffers;  // opaque
+DeviceBuffers* dev_upload(const HostTableSet& h, std::string* err);
+void dev_free(DeviceBuffers* b);
+const DevTableSet& dev_view(const DeviceBuffers* b);
+
+int dev_classify(const DevTableSet& T, int mode, int table_id, const uint32_t* src, const uint32_t* dst,
+                 const uint16_t* sport, const uint16_t* dport, const uint8_t* proto, uint64_t n, uint32_t* out,
+                 unsigned long long* counters, void* stream, std::string* err);
+int dev_classify_linear(const DevTableSet& T, int table_id, const uint32_t* src, const uint32_t* dst,
+                        const uint16_t* dport, const uint8_t* proto, uint64_t n, uint32_t* out, void* stream,
+                        std::string* err);
+int dev_gen(const DevTableSet& T, const GenParams& g, uint64_t n, uint32_t* src, uint32_t* dst, uint16_t* sport,
+            uint16_t* dport, uint8_t* proto, void* stream, std::string* err);
+int dev_conn_queries(const DevTableSet& T, const ConnQueryDev* q_host, size_t n, uint32_t* out_host,
+                     std::string* err);
+int dev_set_device(int dev, std::string* err);
+void* dev_alloc(size_t bytes, std::string* err);
+void dev_release(void* p);
+int dev_memset(void* p, int v, size_t bytes, void* stream, std::string* err);
+int dev_copy_d2h(void* dst, const void* src, size_t bytes, std::string* err);
+int dev_copy_h2d(void* dst, const void* src, size_t bytes, std::string* err);
+int dev_sync(std::string* err);
+
+}  // namespace pg
