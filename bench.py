@@ -1,0 +1,163 @@
+#!/usr/bin/env python3
+"""Benchmark: classified 5-tuples/s of the policy classification path on MI355X.
+
+One step = one pass of the classify kernel over one batch of synthetic 5-tuples already
+resident in HBM (BASELINE.json configs[1] by default: 1k-rule gen-policy-shaped table,
+64M tuples per GPU). Multi-GPU (torchrun, one process per GPU): every rank classifies its
+own shard (tuple index range) against replicated tables -- no data-path collective, weak
+scaling. After the timed region the per-rule hit counters are summed across ranks with one
+RCCL all-reduce (the statscollector path) and its time is reported separately.
+
+Prints ONE JSON line (rank 0). See DESIGN.md §Measurement for the byte accounting.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from vpp_amd import device as D  # noqa: E402
+from vpp_amd import workloads as W  # noqa: E402
+
+METRIC = "classified 5-tuples/sec (Mpps) at 1/2/4/8 GPUs vs rule count; % of HBM peak"
+HBM_PEAK_GBS = 8000.0           # MI355X HBM3E spec (MI355X_MICROARCH.md)
+BYTES_PER_TUPLE = {0: 15, 1: 15, 2: 17}   # 11 B in + 4 B out (+2 B sport in CONN)
+MODE_NAME = {0: "single", 1: "perpod", 2: "conn"}
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--config", type=int, default=2, choices=sorted(W.CONFIGS))
+    p.add_argument("--tuples", type=int, default=0, help="tuples per GPU (default: the config's)")
+    p.add_argument("--counters", action="store_true", help="time with per-rule hit counters on")
+    p.add_argument("--cpu-sample", type=int, default=4 << 20, help="tuples in the CPU-baseline sample")
+    p.add_argument("--no-cpu", action="store_true")
+    return p.parse_args()
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(local)
+    kw = {"n_tuples": a.tuples} if a.tuples else {}
+    w = W.CONFIGS[a.config](local, **kw)
+    e, n = w.engine, w.n_tuples
+    st = w.stats()
+    b = D.TupleBatch(n, with_sport=(w.mode == 2))
+    D.gen_tuples(e, b, index_base=rank * n, **w.gen)
+    out = torch.empty(n, dtype=torch.int32, device="cuda")
+    nslots = e.num_counter_slots()
+    counters = torch.zeros(nslots, dtype=torch.int64, device="cuda")
+    cptr = counters if a.counters else None
+    torch.cuda.synchronize()
+
+    for _ in range(a.warmup):
+        D.classify(e, w.mode, w.table_id, b, out, counters=cptr)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for s0, s1 in evs:
+        s0.record()
+        D.classify(e, w.mode, w.table_id, b, out, counters=cptr)
+        s1.record()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    kern_ms = float(np.mean([s0.elapsed_time(s1) for s0, s1 in evs]))
+    if world > 1:
+        t = torch.tensor([wall], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        wall = float(t.item())
+    ms_per_step = wall * 1e3 / a.steps
+    total_tuples = n * world * a.steps
+    mpps = total_tuples / wall / 1e6
+
+    # statscollector path: one RCCL all-reduce of the per-rule hit counters
+    allreduce_ms = None
+    if world > 1:
+        D.classify(e, w.mode, w.table_id, b, out, counters=counters)
+        torch.cuda.synchronize()
+        dist.barrier()
+        t1 = time.perf_counter()
+        dist.all_reduce(counters)
+        torch.cuda.synchronize()
+        allreduce_ms = (time.perf_counter() - t1) * 1e3
+
+    achieved = n * BYTES_PER_TUPLE[w.mode] / (kern_ms * 1e-3) / 1e9
+    line = {
+        "metric": METRIC, "value": round(mpps, 1), "unit": "Mpps", "n_gpus": world, "steps": a.steps,
+        "warmup": a.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "u32", "data": "synthetic (device-generated, counter-based splitmix64)",
+        "config": {"workload": "config%d: %s" % (a.config, w.desc), "mode": MODE_NAME[w.mode],
+                   "tuples_per_gpu": n, "rules": st["rules"], "tables": st["tables"], "parallelism": "dp%d" % world,
+                   "counters": bool(a.counters)},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                     "bytes_per_tuple": BYTES_PER_TUPLE[w.mode], "kernel_ms": round(kern_ms, 4)},
+    }
+    if allreduce_ms is not None:
+        line["counter_allreduce_ms"] = round(allreduce_ms, 3)
+    if rank == 0 and world == 1 and not a.no_cpu:
+        line["cpu_baseline"], line["parity_sample"] = cpu_baseline(w, b, out, a.cpu_sample)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(w, b, out, k):
+    """The oracle's evalACL/testConnection (oracle/oracle.c) timed on this host's cores over
+    the first k tuples of the same workload; also checks the GPU verdicts on that sample."""
+    from oracle import fast  # cpu_baseline leg: the checker, never the thing measured on GPU
+
+    k = min(k, b.n)
+    src, dst, sport, dport, proto = b.numpy(k)
+    got = out[:k].cpu().numpy().view(np.uint32)
+    e = w.engine
+    threads = min(16, os.cpu_count() or 1)
+    names = e.ACLNames()
+    ora = [fast.OraACL(e.GetACLByName(x)["rules"]) for x in names]
+    if w.mode == 0:
+        t0 = time.perf_counter()
+        act, idx = fast.eval_acl(ora[w.table_id], src, dst, dport, proto, threads=threads)
+        dt = time.perf_counter() - t0
+        ok = bool(((got >> 30) == act.astype(np.uint32)).all())
+        kind = "evalACL over the same ACL (rules pre-parsed), %d threads" % threads
+    else:
+        raise NotImplementedError("cpu baseline for mode %d" % w.mode)
+    # reference-faithful variant (CIDR strings parsed per rule visit, one thread), small sample
+    kf = min(k, 1 << 16)
+    rules = e.GetACLByName(names[w.table_id])["rules"] if w.mode == 0 else None
+    t0 = time.perf_counter()
+    fast.eval_acl_faithful(rules, src[:kf], dst[:kf], dport[:kf], proto[:kf])
+    dtf = time.perf_counter() - t0
+    return ({"value": round(k / dt / 1e6, 3), "unit": "Mpps", "cores": threads, "kind": "port",
+             "sample": "first %d tuples of the same workload; %s" % (k, kind),
+             "faithful_1thread_mpps": round(kf / dtf / 1e6, 4)},
+            {"tuples": k, "bit_exact_actions": ok})
+
+
+if __name__ == "__main__":
+    main()

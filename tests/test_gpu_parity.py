@@ -1,0 +1,242 @@
+"""Bit-exact parity of the HIP kernels against the CPU oracle (oracle/oracle.c, pinned to
+the reference's KATs through oracle/aclengine.py).
+
+Verdict = (ACLAction or ConnAction, deciding counter slot); slots map back to
+(ACL, rule index) through pg_slot_info, so "matched rule index" parity is checked too.
+"""
+import random
+
+import numpy as np
+import pytest
+import torch
+
+import acl_fuzz as fz
+from oracle import fast
+
+pytestmark = pytest.mark.gpu
+
+from vpp_amd import device as D  # noqa: E402
+from vpp_amd import renderer as R  # noqa: E402
+from vpp_amd._capi import MODE_CONN, MODE_PERPOD, MODE_SINGLE  # noqa: E402
+
+
+def make_engine(acls_by_if, pods=(), node_if="VXLAN-BVI"):
+    """acls_by_if: {ifname: (inbound rules|None, outbound rules|None)} -> Engine."""
+    e = R.Engine(0)
+    e.SetMainInterfaceName("GbE")
+    e.SetVxlanBVIIfName(node_if)
+    e.SetHostInterconnectIfName("VPP-Host")
+    for pod, ip, ifn, another in pods:
+        if ifn:
+            e.SetPodIfName(pod, ifn)
+        e.RegisterPod(pod, ip, another)
+    ops = []
+    for ifn, (inb, outb) in sorted(acls_by_if.items()):
+        if inb is not None:
+            ops.append(("config/vpp/acls/v2/acl/in-" + ifn, {"name": "in-" + ifn, "rules": inb, "ingress": [ifn],
+                                                             "egress": []}))
+        if outb is not None:
+            ops.append(("config/vpp/acls/v2/acl/out-" + ifn, {"name": "out-" + ifn, "rules": outb, "ingress": [],
+                                                              "egress": [ifn]}))
+    e.ApplyTxn(True, ops)
+    e.sync()
+    return e
+
+
+def slot_map(e):
+    """(table id, rule index) -> slot; (table, -1) -> default slot; (-1,-1) no ACL."""
+    m = {}
+    for s in range(e.num_counter_slots()):
+        m[e.slot_info(s)] = s
+    return m
+
+
+def run_single(e, tid, tup, counters=False):
+    n = len(tup[0])
+    b = D.TupleBatch.from_numpy(*tup)
+    out = torch.empty(n, dtype=torch.int32, device="cuda")
+    cnt = None
+    if counters:
+        D.reset_counters(e)
+        cnt = D.counters_device_ptr(e)
+    D.classify(e, MODE_SINGLE, tid, b, out, counters=cnt)
+    torch.cuda.synchronize()
+    return out.cpu().numpy().view(np.uint32), b
+
+
+def expected_single(e, tid, rules, tup):
+    src, dst, sport, dport, proto = tup
+    a, i = fast.eval_acl(fast.OraACL(rules), src, dst, dport, proto)
+    sm = slot_map(e)
+    slots = np.array([sm[(tid, int(x))] if x >= 0 else sm[(tid, -1)] for x in i], np.uint32)
+    return a.astype(np.uint32), slots
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_single_mode_random_acls_bit_exact(seed):
+    rnd = random.Random(seed)
+    acls = {"if%d" % k: (None, fz.rand_acl(rnd, rnd.choice([1, 5, 30, 120]), fz.ANCHORS, weird=True,
+                                           tail=rnd.choice([None, "deny", "permit"]))) for k in range(3)}
+    e = make_engine(acls)
+    tup = fz.rand_tuples(np.random.default_rng(seed), 40000 + seed, fz.ANCHORS, any_pct=0.03)
+    for ifn, (_, rules) in acls.items():
+        tid = e.table_id("out-" + ifn)
+        got, _ = run_single(e, tid, tup)
+        ea, es = expected_single(e, tid, rules, tup)
+        assert ((got >> 30) == ea).all(), np.nonzero((got >> 30) != ea)[0][:10]
+        assert ((got & 0x3FFFFFFF) == es).all(), np.nonzero((got & 0x3FFFFFFF) != es)[0][:10]
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_linear_kernel_equals_indexed_kernel(seed):
+    rnd = random.Random(100 + seed)
+    rules = fz.rand_acl(rnd, 200, fz.ANCHORS, weird=True, tail="deny")
+    e = make_engine({"x": (None, rules)})
+    tid = e.table_id("out-x")
+    tup = fz.rand_tuples(np.random.default_rng(seed), 100003, fz.ANCHORS, any_pct=0.02)
+    got, b = run_single(e, tid, tup)
+    lin = torch.empty(b.n, dtype=torch.int32, device="cuda")
+    D.classify_linear(e, tid, b, lin)
+    torch.cuda.synchronize()
+    assert (lin.cpu().numpy().view(np.uint32) == got).all()
+
+
+def test_counters_equal_verdict_histogram_and_oracle():
+    rnd = random.Random(7)
+    rules = fz.rand_acl(rnd, 60, fz.ANCHORS, weird=False, tail="deny")
+    e = make_engine({"x": (None, rules)})
+    tid = e.table_id("out-x")
+    tup = fz.rand_tuples(np.random.default_rng(7), 300000, fz.ANCHORS)
+    got, _ = run_single(e, tid, tup, counters=True)
+    cnt = D.read_counters(e)
+    hist = np.bincount(got & 0x3FFFFFFF, minlength=len(cnt))
+    assert (cnt == hist).all()
+    _, es = expected_single(e, tid, rules, tup)
+    assert (np.bincount(es, minlength=len(cnt)) == cnt).all()
+
+
+@pytest.mark.parametrize("n", [0, 1, 2, 3, 4, 5, 7, 9, 255, 257, 1023, 4099])
+def test_ragged_sizes_and_tails(n):
+    rnd = random.Random(n)
+    rules = fz.rand_acl(rnd, 25, fz.ANCHORS, weird=True, tail="deny")
+    e = make_engine({"x": (None, rules)})
+    tid = e.table_id("out-x")
+    tup = fz.rand_tuples(np.random.default_rng(n), max(n, 1), fz.ANCHORS)
+    tup = tuple(a[:n] for a in tup)
+    if n == 0:
+        b = D.TupleBatch(0)
+        out = torch.empty(0, dtype=torch.int32, device="cuda")
+        D.classify(e, MODE_SINGLE, tid, b, out)
+        return
+    got, _ = run_single(e, tid, tup)
+    ea, es = expected_single(e, tid, rules, tup)
+    assert ((got >> 30) == ea).all() and ((got & 0x3FFFFFFF) == es).all()
+
+
+def test_misaligned_pointers_take_scalar_path():
+    rnd = random.Random(11)
+    rules = fz.rand_acl(rnd, 40, fz.ANCHORS, weird=True, tail="deny")
+    e = make_engine({"x": (None, rules)})
+    tid = e.table_id("out-x")
+    tup = fz.rand_tuples(np.random.default_rng(11), 10001, fz.ANCHORS)
+    b = D.TupleBatch.from_numpy(*tup)
+    out = torch.zeros(b.n, dtype=torch.int32, device="cuda")
+    D.classify(e, MODE_SINGLE, tid, b, out, offset=1)  # every pointer off by one element
+    torch.cuda.synchronize()
+    got = out.cpu().numpy().view(np.uint32)[1:]
+    ea, es = expected_single(e, tid, rules, tuple(a[1:] for a in tup))
+    assert ((got >> 30) == ea).all() and ((got & 0x3FFFFFFF) == es).all()
+
+
+def _topology(rnd, n_pods=12, weird=False):
+    pods = []
+    acls = {}
+    for k in range(n_pods):
+        ip = 0x0A0A0000 | (k + 1)
+        another = k >= n_pods - 2
+        ifn = "tap%d" % k if not another else None
+        pods.append(("ns/p%d" % k, "%d.%d.%d.%d" % (ip >> 24, ip >> 16 & 255, ip >> 8 & 255, ip & 255), ifn, another))
+        if ifn:
+            inb = fz.rand_acl(rnd, rnd.randint(0, 8), fz.ANCHORS + [ip], weird) if rnd.random() < 0.6 else None
+            outb = fz.rand_acl(rnd, rnd.randint(0, 12), fz.ANCHORS + [ip], weird, tail="deny") if rnd.random() < 0.7 \
+                else None
+            if inb is not None and rnd.random() < 0.5:
+                inb = [{"action": 2, "src": "", "dst": ""}]          # reflective ACL
+            acls[ifn] = (inb, outb)
+    acls["VXLAN-BVI"] = (fz.rand_acl(rnd, 3, fz.ANCHORS, weird) if rnd.random() < 0.5 else None,
+                         fz.rand_acl(rnd, 20, fz.ANCHORS, weird, tail="permit"))
+    return pods, acls
+
+
+def _resolve(e, pods, ips):
+    """IPv4 -> interface index as the device does it (local pod TAP else node interface)."""
+    names = {}
+    for pod, ip, ifn, another in pods:
+        if not another:
+            names[fz_ip(ip)] = ifn
+    return names
+
+
+def fz_ip(s):
+    a, b, c, d = (int(x) for x in s.split("."))
+    return (a << 24) | (b << 16) | (c << 8) | d
+
+
+def _oracle_world(e, acls):
+    names = sorted(n for n in e.ACLNames())
+    ora = [fast.OraACL(e.GetACLByName(n)["rules"]) for n in names]
+    tid = {n: i for i, n in enumerate(names)}
+    return names, ora, tid
+
+
+@pytest.mark.parametrize("seed", range(5))
+def test_conn_and_perpod_modes_random_topology(seed):
+    rnd = random.Random(1000 + seed)
+    pods, acls = _topology(rnd, weird=seed % 2 == 1)
+    e = make_engine(acls, pods)
+    names, ora, tid = _oracle_world(e, acls)
+    assert [e.table_id(n) for n in names] == list(range(len(names)))
+    pod_ips = [fz_ip(p[1]) for p in pods]
+    n = 60000
+    rng = np.random.default_rng(seed)
+    tup = list(fz.rand_tuples(rng, n, fz.ANCHORS + pod_ips))
+    for k in (0, 1):  # 60 % of endpoints are pods
+        m = rng.random(n) < 0.6
+        tup[k][m] = np.array(pod_ips, np.uint32)[rng.integers(0, len(pod_ips), int(m.sum()))]
+    tup = tuple(tup)
+    local = {fz_ip(ip): ifn for pod, ip, ifn, another in pods if not another}
+    ifnames = sorted(set(list(acls) + [p[2] for p in pods if p[2]] + ["GbE", "VPP-Host"]))
+    ifx = {x: i for i, x in enumerate(ifnames)}
+    node = ifx["VXLAN-BVI"]
+    if_in = [tid.get("in-" + x, -1) for x in ifnames]
+    if_out = [tid.get("out-" + x, -1) for x in ifnames]
+    sif = np.array([ifx[local[int(s)]] if int(s) in local else node for s in tup[0]], np.int32)
+    dif = np.array([ifx[local[int(d)]] if int(d) in local else node for d in tup[1]], np.int32)
+    src, dst, sport, dport, proto = tup
+    b = D.TupleBatch.from_numpy(*tup)
+    sm = slot_map(e)
+
+    # CONN
+    out = torch.empty(n, dtype=torch.int32, device="cuda")
+    D.classify(e, MODE_CONN, -1, b, out)
+    torch.cuda.synchronize()
+    got = out.cpu().numpy().view(np.uint32)
+    conn, lt, li = fast.test_connection(ora, if_in, if_out, sif, dif, src, dst, sport, dport, proto)
+    exp_slot = np.array([sm[(int(t), int(i))] if t >= 0 and i >= 0 else (sm[(int(t), -1)] if t >= 0 else sm[(-1, -1)])
+                         for t, i in zip(lt, li)], np.uint32)
+    assert ((got >> 30) == conn.astype(np.uint32)).all(), np.nonzero((got >> 30) != conn)[0][:10]
+    assert ((got & 0x3FFFFFFF) == exp_slot).all()
+
+    # PERPOD: evalACL(outbound ACL of dst's interface)
+    D.classify(e, MODE_PERPOD, -1, b, out)
+    torch.cuda.synchronize()
+    got = out.cpu().numpy().view(np.uint32)
+    ea = np.empty(n, np.int64)
+    es = np.empty(n, np.int64)
+    for t_if in np.unique(dif):
+        m = dif == t_if
+        t = if_out[t_if]
+        a, i = fast.eval_acl(ora[t] if t >= 0 else None, src[m], dst[m], dport[m], proto[m])
+        ea[m] = a
+        es[m] = [sm[(t, int(x))] if t >= 0 and x >= 0 else (sm[(t, -1)] if t >= 0 else sm[(-1, -1)]) for x in i]
+    assert ((got >> 30) == ea).all() and ((got & 0x3FFFFFFF) == es).all()

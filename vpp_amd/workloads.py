@@ -1,0 +1,203 @@
+"""Synthetic workloads of BASELINE.json's configs, built through the
+product's own renderer / ACL-ingestion path. Inputs are synthetic (no datasets exist for
+this path); shapes follow the reference's own fixtures and perf generator:
+
+  config 1  renderer unit-test scenario (acl_renderer_test.go TestCombinedRules, first txn),
+            connection mode, 1M tuples
+  config 2  1k-rule single table shaped like tests/policy/perf/gen-policy.py (/16-/24 CIDRs
+            under (i+0x100)<<16 minus five /24-/32 excepts, x 20 TCP/UDP ports), first 999
+            generated rules + deny-the-rest, 64M tuples (bench.py's default)
+  config 3  1k pods / 10 namespaces / per-app policies -> local tables + global table,
+            per-pod (egress interface) mode
+  config 4  100k-rule ACL ingested directly (vpp_acl key space), disjoint src prefixes,
+            first-match depth Zipf(1.1), 5 % no-match
+  config 5  config-3 topology in connection mode with per-rule hit counters
+"""
+import random
+
+import numpy as np
+
+from . import renderer as R
+from ._capi import MODE_CONN, MODE_PERPOD, MODE_SINGLE
+
+SEEDS = {1: 0xC0DE0001, 2: 0xC0DE0002, 3: 0xC0DE0003, 4: 0xC0DE0004, 5: 0xC0DE0005}
+POPULAR_PORTS = [22, 53, 67, 80, 81, 161, 162, 443, 514, 8080]
+
+
+def ip_str(v):
+    return "%d.%d.%d.%d" % (v >> 24 & 255, v >> 16 & 255, v >> 8 & 255, v & 255)
+
+
+def ip_u32(s):
+    a, b, c, d = (int(x) for x in s.split("."))
+    return (a << 24) | (b << 16) | (c << 8) | d
+
+
+def mask_ip(ip, plen):
+    return ip & ((0xFFFFFFFF << (32 - plen)) & 0xFFFFFFFF) if plen else 0
+
+
+def subtract_subnet(n1, n2):
+    """IPv4 form of the configurator's subtractSubnet (configurator_impl.go:562-594)."""
+    (ip1, l1), (ip2, l2) = n1, n2
+    if l1 > l2:
+        return [n1] if mask_ip(ip1, l2) != mask_ip(ip2, l2) else []
+    if l1 == l2:
+        return [n1] if ip1 != ip2 else []
+    if mask_ip(ip2, l1) != mask_ip(ip1, l1):
+        return [n1]
+    out = []
+    for bit in range(l1, l2):
+        sub = mask_ip(ip2, bit + 1) ^ (1 << (31 - bit))
+        out.append((sub, bit + 1))
+    return out
+
+
+class Workload:
+    def __init__(self, config, engine, mode, table_id, gen, n_tuples, desc, renderer=None):
+        self.config, self.engine, self.mode, self.table_id = config, engine, mode, table_id
+        self.gen, self.n_tuples, self.desc, self.renderer = gen, n_tuples, desc, renderer
+
+    def stats(self):
+        e = self.engine
+        nt = e.num_tables()
+        return {"tables": nt, "rules": e.num_counter_slots() - nt - 2}
+
+
+def _new_engine(device):
+    e = R.Engine(device)
+    e.SetMainInterfaceName("GbE")
+    e.SetVxlanBVIIfName("VXLAN-BVI")
+    e.SetHostInterconnectIfName("VPP-Host")
+    return e
+
+
+# ---- config 1 ------------------------------------------------------------------------
+TESTDATA_PODS = ["default/pod1", "default/pod2", "default/pod3", "default/pod4", "default/pod5", "namespace2/pod6"]
+TESTDATA_IPS = ["10.10.1.1", "10.10.1.2", "10.10.2.1", "10.10.2.2", "10.10.2.3", "10.10.10.1"]
+
+
+def _rule(a, s, d, p, dp):
+    return R.ContivRule(a, R.IPNet(s), R.IPNet(d), p, 0, dp)
+
+
+def config1(device=0, n_tuples=1 << 20):
+    """TestCombinedRules (acl_renderer_test.go:447-553) tables, testdata.go:172-256 rules."""
+    P, D = R.ActionPermit, R.ActionDeny
+    deny = _rule(D, "", "", R.ANY, 0)
+    pod1_in = [_rule(P, "", "", R.UDP, 161), deny]                                  # Ts7.Pod1Ingress[1:]
+    pod1_eg = [_rule(P, "10.0.0.0/8", "", R.UDP, 53), _rule(P, "192.168.0.0/16", "", R.UDP, 514)]
+    pod3_in = [_rule(P, "", "10.10.1.1/32", R.UDP, 0), _rule(P, "", "", R.TCP, 22), deny]
+    pod3_eg = [_rule(P, "10.0.0.0/8", "", R.TCP, 80), _rule(P, "10.0.0.0/8", "", R.TCP, 443),
+               _rule(P, "", "", R.UDP, 67), deny]
+    e = _new_engine(device)
+    e.SetPodIfName("default/pod1", "node1-tap1")
+    e.SetPodIfName("default/pod3", "node1-tap3")
+    e.RegisterPod("default/pod1", "10.10.1.1", False)
+    e.RegisterPod("default/pod3", "10.10.2.1", False)
+    e.RegisterPod("namespace2/pod6", "10.10.10.1", True)
+    r = R.Renderer(e)
+    t = r.NewTxn(True)
+    t.Render("default/pod1", R.IPNet.host("10.10.1.1"), pod1_in, pod1_eg, False)
+    t.Render("default/pod3", R.IPNet.host("10.10.2.1"), pod3_in, pod3_eg, False)
+    err = t.Commit()
+    assert err is None, err
+    pool = [ip_u32(x) for x in TESTDATA_IPS] * 4 + [ip_u32(x) for x in ("8.8.8.8", "10.10.50.1", "192.168.1.1")] * 6
+    gen = dict(seed=SEEDS[1], ip_pool=np.array(pool, np.uint32), pool_pct=70, dst_pool_pct=70,
+               port_pool=np.array(POPULAR_PORTS, np.uint16), port_pool_pct=50, tcp_pct=45, udp_pct=45)
+    return Workload(1, e, MODE_CONN, -1, gen, n_tuples, "TestCombinedRules tables, testConnection by IP", r)
+
+
+# ---- config 2 ------------------------------------------------------------------------
+def gen_policy_rules(seed, max_rules=999, num_excepts=5, num_ports=20):
+    """tests/policy/perf/gen-policy.py:35-60 ipBlocks x ports, turned into ContivRules the way
+    the configurator does for an ingress policy (SrcNetwork = subtracted block piece)."""
+    rnd = random.Random(seed)
+    ports = [(R.TCP if rnd.randint(0, 1) == 0 else R.UDP, rnd.randint(0, 65535)) for _ in range(num_ports)]
+    rules = []
+    i = 0
+    while len(rules) < max_rules:
+        prefix = (i + 0x100) << 16
+        cidr = rnd.randint(prefix, prefix | 0xFFFF)
+        ml = rnd.randint(16, 24)
+        cidr = mask_ip(cidr, ml)
+        excepts = []
+        for _ in range(num_excepts):
+            ex = rnd.randint(cidr, cidr | ((1 << (32 - ml)) - 1))
+            el = rnd.randint(24, 32)
+            excepts.append((mask_ip(ex, el), el))
+        pieces = [(cidr, ml)]
+        for ex in excepts:
+            pieces = [q for p in pieces for q in subtract_subnet(p, ex)]
+        for ip, pl in pieces:
+            for proto, port in ports:
+                rules.append(R.ContivRule(R.ActionPermit, R.IPNet("%s/%d" % (ip_str(ip), pl)), R.IPNet(), proto, 0,
+                                          port))
+        i += 1
+    return rules[:max_rules]
+
+
+def config2(device=0, n_tuples=64 << 20):
+    e = _new_engine(device)
+    pod = "default/db-0"
+    e.SetPodIfName(pod, "node1-tap-db0")
+    e.RegisterPod(pod, "10.1.0.10", False)
+    r = R.Renderer(e)
+    rules = gen_policy_rules(SEEDS[2]) + [R.ContivRule(R.ActionDeny, R.IPNet(), R.IPNet(), R.ANY, 0, 0)]
+    t = r.NewTxn(True)
+    t.Render(pod, R.IPNet.host("10.1.0.10"), [], rules, False)
+    err = t.Commit()
+    assert err is None, err
+    acl = e.GetOutboundACL("node1-tap-db0")
+    tid = e.table_id(acl["name"])
+    gen = dict(seed=SEEDS[2], table_id=tid, inside_pct=50, tcp_pct=45, udp_pct=45)
+    return Workload(2, e, MODE_SINGLE, tid, gen, n_tuples, "gen-policy 1k-rule table (%d rules)" % len(acl["rules"]),
+                    r)
+
+
+# ---- config 4 ------------------------------------------------------------------------
+def zipf_cdf(n, s=1.1):
+    w = 1.0 / np.power(np.arange(1, n + 1, dtype=np.float64), s)
+    c = np.cumsum(w)
+    c /= c[-1]
+    u = np.minimum(np.floor(c * 4294967296.0), 4294967295.0).astype(np.uint64)
+    u[-1] = 4294967295
+    return u.astype(np.uint32)
+
+
+def big_acl_rules(n_rules, seed):
+    """Disjoint src prefixes (/26../32) packed in 10.0.0.0/8, random L4 section and action."""
+    rnd = random.Random(seed)
+    rules = []
+    addr = 10 << 24
+    for _ in range(n_rules):
+        pl = rnd.randint(26, 32)
+        size = 1 << (32 - pl)
+        addr = (addr + size - 1) & ~(size - 1)
+        src = "%s/%d" % (ip_str(addr), pl)
+        addr += size
+        kind = rnd.random()
+        rule = {"action": rnd.choice([0, 1]), "src": src, "dst": ""}
+        if kind < 0.4:
+            lo = rnd.randint(1, 65000)
+            rule["tcp"] = {"src": [0, 65535], "dst": [lo, lo + rnd.choice([0, 0, 10, 500])]}
+        elif kind < 0.8:
+            lo = rnd.randint(1, 65000)
+            rule["udp"] = {"src": [0, 65535], "dst": [lo, lo + rnd.choice([0, 0, 10, 500])]}
+        rules.append(rule)
+    assert addr <= (11 << 24)
+    return rules
+
+
+def config4(device=0, n_tuples=64 << 20, n_rules=100000):
+    e = _new_engine(device)
+    acl = {"name": "contiv-policy-bigtable", "ingress": [], "egress": ["node1-tap-big"],
+           "rules": big_acl_rules(n_rules, SEEDS[4])}
+    e.ApplyTxn(True, [("config/vpp/acls/v2/acl/" + acl["name"], acl)])
+    tid = e.table_id(acl["name"])
+    gen = dict(seed=SEEDS[4], table_id=tid, inside_pct=95, nomatch_pct=5, zipf_cdf=zipf_cdf(n_rules),
+               tcp_pct=45, udp_pct=45)
+    return Workload(4, e, MODE_SINGLE, tid, gen, n_tuples, "100k-rule ACL, Zipf(1.1) first-match depth")
+
+
+CONFIGS = {1: config1, 2: config2, 4: config4}
