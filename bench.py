@@ -143,7 +143,10 @@ def cpu_baseline(w, b, out, k):
         t0 = time.perf_counter()
         act, idx = fast.eval_acl(ora[w.table_id], src, dst, dport, proto, threads=threads)
         dt = time.perf_counter() - t0
-        ok = bool(((got >> 30) == act.astype(np.uint32)).all())
+        base = e.slot_of_rule(w.table_id, 0)
+        dflt = e.slot_of_rule(w.table_id, -1)
+        slot = np.where(idx >= 0, base + idx.astype(np.int64), dflt).astype(np.uint32)
+        ok = bool(((got >> 30) == act.astype(np.uint32)).all() and ((got & 0x3FFFFFFF) == slot).all())
         kind = "evalACL over the same ACL (rules pre-parsed), %d threads" % threads
     else:
         raise NotImplementedError("cpu baseline for mode %d" % w.mode)
@@ -156,7 +159,7 @@ def cpu_baseline(w, b, out, k):
     return ({"value": round(k / dt / 1e6, 3), "unit": "Mpps", "cores": threads, "kind": "port",
              "sample": "first %d tuples of the same workload; %s" % (k, kind),
              "faithful_1thread_mpps": round(kf / dtf / 1e6, 4)},
-            {"tuples": k, "bit_exact_actions": ok})
+            {"tuples": k, "bit_exact_action_and_rule_index": ok})
 
 
 if __name__ == "__main__":

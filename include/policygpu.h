@@ -179,6 +179,8 @@ int pg_num_counter_slots(pg_ctx* ctx);
 /* global rule slot -> (table id, rule index in its ACL); rule index -1 for a table's
  * default-deny slot; table id -1 for the "no ACL" (permit) slot */
 int pg_slot_info(pg_ctx* ctx, uint32_t slot, int32_t* table_id, int32_t* rule_index);
+/* table -> (first rule slot, rules, default-deny slot) */
+int pg_table_info(pg_ctx* ctx, int table_id, uint32_t* rule_base, uint32_t* n_rules, uint32_t* default_slot);
 
 int pg_classify(pg_ctx* ctx, int mode, int table_id, const pg_tuple_soa* tuples, uint64_t n, uint32_t* out,
                 uint64_t* counters, void* hip_stream);

@@ -149,3 +149,35 @@ def test_random_renderer_transactions_match_oracle(seed):
         assert product_acls(prod.engine) == oracle_acls(ora.engine), step
         assert prod.num_acl_changes() == ora.num_acl_changes()
         assert prod.committed_txns() == ora.committed_txns()
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_acl_ingestion_roundtrip(seed):
+    """ApplyTxn (vpp_acl key space) keeps every field evalACL reads, incl. missing ranges."""
+    import acl_fuzz as fz
+    from vpp_amd import renderer as R
+    rnd = random.Random(seed)
+    e = R.Engine(0)
+    acls = []
+    for k in range(3):
+        rules = fz.rand_acl(rnd, 30, fz.ANCHORS, weird=True)
+        acls.append({"name": "a%d" % k, "rules": rules, "ingress": ["if%d" % k], "egress": []})
+    e.ApplyTxn(True, [("config/vpp/acls/v2/acl/" + a["name"], a) for a in acls])
+    for a in acls:
+        got = e.GetACLByName(a["name"])
+        for r0, r1 in zip(a["rules"], got["rules"]):
+            assert r1["action"] == r0["action"] and r1["src"] == r0["src"] and r1["dst"] == r0["dst"]
+            for f in ("tcp", "udp"):
+                if r0.get(f) is None:
+                    assert r1[f] is None
+                else:
+                    assert r1[f] == {"src": r0[f].get("src"), "dst": r0[f].get("dst")}
+            for f, d in (("macip", False), ("ip_rule", True), ("ip", True), ("icmp", False)):
+                assert r1[f] == r0.get(f, d)
+    with pytest.raises(R.PolicyError):
+        e.ApplyTxn(False, [("config/vpp/interfaces/x", None)])
+    with pytest.raises(R.PolicyError):
+        e.ApplyTxn(False, [("config/vpp/acls/v2/acl/missing", None)])
+    with pytest.raises(R.PolicyError):
+        e.ApplyTxn(False, [("config/vpp/acls/v2/acl/noifs", {"name": "noifs", "rules": [], "ingress": [],
+                                                             "egress": []})])

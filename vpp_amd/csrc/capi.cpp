@@ -264,8 +264,10 @@ int pg_acl_json(pg_ctx* ctx, const char* acl_name, char* buf, size_t cap) {
     s += "],\"rules\":[";
     auto l4 = [](const L4Section& x) {
         if (!x.present) return std::string("null");
-        return "{\"src\":[" + std::to_string(x.src.lower) + "," + std::to_string(x.src.upper) + "],\"dst\":[" +
-               std::to_string(x.dst.lower) + "," + std::to_string(x.dst.upper) + "]}";
+        auto rng = [](bool has, const PortRange& p) {
+            return has ? "[" + std::to_string(p.lower) + "," + std::to_string(p.upper) + "]" : std::string("null");
+        };
+        return "{\"src\":" + rng(x.has_src, x.src) + ",\"dst\":" + rng(x.has_dst, x.dst) + "}";
     };
     for (size_t i = 0; i < a.rules.size(); i++) {
         const AclRule& r = a.rules[i];
@@ -359,15 +361,31 @@ int pg_slot_info(pg_ctx* ctx, uint32_t slot, int32_t* table_id, int32_t* rule_in
     return PG_OK;
 }
 
+int pg_table_info(pg_ctx* ctx, int table_id, uint32_t* rule_base, uint32_t* n_rules, uint32_t* default_slot) {
+    if (!ctx) return PG_EINVAL;
+    int rc = pg_sync_tables(ctx);
+    if (rc) return rc;
+    const DevTableSet& T = *ctx->eng.view();
+    if (table_id < 0 || (uint32_t)table_id >= T.n_tables) return fail(ctx, PG_EINVAL, "table id out of range");
+    uint32_t base = 0;
+    for (int t = 0; t < table_id; t++) base += (uint32_t)ctx->eng.by_name[ctx->eng.table_names[t]]->rules.size();
+    if (rule_base) *rule_base = base;
+    if (n_rules) *n_rules = (uint32_t)ctx->eng.by_name[ctx->eng.table_names[table_id]]->rules.size();
+    if (default_slot) *default_slot = T.n_rules + (uint32_t)table_id;
+    return PG_OK;
+}
+
 int pg_classify(pg_ctx* ctx, int mode, int table_id, const pg_tuple_soa* t, uint64_t n, uint32_t* out,
                 uint64_t* counters, void* stream) {
-    if (!ctx || !t || !out || mode < 0 || mode > 2) return PG_EINVAL;
+    if (!ctx || !t || mode < 0 || mode > 2) return PG_EINVAL;
     GUARD_BEGIN
     int rc = ctx->eng.sync();
     if (rc) return rc;
     const DevTableSet& T = *ctx->eng.view();
     if (mode == PG_MODE_SINGLE && (table_id < 0 || (uint32_t)table_id >= T.n_tables))
         return fail(ctx, PG_EINVAL, "table id out of range");
+    if (n == 0) return PG_OK;
+    if (!out) return fail(ctx, PG_EINVAL, "null output");
     if (!t->src_ip || !t->dst_ip || !t->dst_port || !t->proto || (mode == PG_MODE_CONN && !t->src_port))
         return fail(ctx, PG_EINVAL, "missing tuple field");
     std::string err;

@@ -230,6 +230,16 @@ class Engine:
         self._ck(lib.pg_slot_info(self.h, slot, C.byref(t), C.byref(r)))
         return t.value, r.value
 
+    def table_info(self, tid):
+        b, n, d = C.c_uint32(), C.c_uint32(), C.c_uint32()
+        self._ck(lib.pg_table_info(self.h, tid, C.byref(b), C.byref(n), C.byref(d)))
+        return b.value, n.value, d.value
+
+    def slot_of_rule(self, tid, idx):
+        """counter slot of rule ``idx`` of table ``tid`` (idx -1: the table's default deny)."""
+        base, n, dflt = self.table_info(tid)
+        return base + idx if idx >= 0 else dflt
+
     # Connection* (aclengine_mock.go:273-420), testConnection evaluated on the GPU
     def connections(self, queries):
         """queries: list of (kind, a, b, proto, sport, dport) with kind in
