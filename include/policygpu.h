@@ -182,8 +182,19 @@ int pg_slot_info(pg_ctx* ctx, uint32_t slot, int32_t* table_id, int32_t* rule_in
 /* table -> (first rule slot, rules, default-deny slot) */
 int pg_table_info(pg_ctx* ctx, int table_id, uint32_t* rule_base, uint32_t* n_rules, uint32_t* default_slot);
 
+/* classification structure of a table: flags (1 cross, 2 dst lists, 4 candidate mode,
+ * 8 linear fallback), blob bytes, src / key equivalence classes */
+int pg_table_stats(pg_ctx* ctx, int table_id, uint32_t* flags, uint32_t* blob_bytes, uint32_t* n_src_classes,
+                   uint32_t* n_key_classes);
+
 int pg_classify(pg_ctx* ctx, int mode, int table_id, const pg_tuple_soa* tuples, uint64_t n, uint32_t* out,
                 uint64_t* counters, void* hip_stream);
+
+/* TESTS ONLY -- never on the classify path: walk one ACL's compiled classification blob on
+ * the host (the same walk code the kernels instantiate) for n host tuples, so the table
+ * compiler can be checked against the oracle without a GPU. Does not touch the device. */
+int pg_debug_walk_blob(pg_ctx* ctx, const char* acl_name, const uint32_t* src, const uint32_t* dst,
+                       const uint16_t* dst_port, const uint8_t* proto, uint64_t n, uint32_t* out);
 /* reference-shaped linear-scan kernel (K1) on one table, for validation and comparison */
 int pg_classify_linear(pg_ctx* ctx, int table_id, const pg_tuple_soa* tuples, uint64_t n, uint32_t* out,
                        void* hip_stream);

@@ -101,6 +101,9 @@ _SIGS = {
     "pg_slot_info": (C.c_int, [_P, C.c_uint32, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
     "pg_table_info": (C.c_int, [_P, C.c_int, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]),
     "pg_classify":(C.c_int, [_P, C.c_int, C.c_int, C.POINTER(pg_tuple_soa), C.c_uint64, _P, _P, _P]),
+    "pg_table_stats": (C.c_int, [_P, C.c_int, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.POINTER(C.c_uint32),
+                                 C.POINTER(C.c_uint32)]),
+    "pg_debug_walk_blob": (C.c_int, [_P, C.c_char_p, _P, _P, _P, _P, C.c_uint64, _P]),
     "pg_classify_linear": (C.c_int, [_P, C.c_int, C.POINTER(pg_tuple_soa), C.c_uint64, _P, _P]),
     "pg_counters_device": (_P, [_P]),
     "pg_reset_counters": (C.c_int, [_P, _P]),

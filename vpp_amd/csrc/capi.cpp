@@ -5,6 +5,7 @@
 #include <stdexcept>
 
 #include "../../include/policygpu.h"
+#include "blobwalk.hpp"
 #include "engine.hpp"
 
 using namespace pg;
@@ -135,32 +136,32 @@ const char* pg_last_error(const pg_ctx* ctx) { return ctx ? ctx->eng.last_error.
 int pg_set_pod_if_name(pg_ctx* ctx, const char* ns, const char* name, const char* if_name) {
     if (!ctx || !ns || !name || !if_name) return PG_EINVAL;
     ctx->eng.ifaces.pod_if[PodID{ns, name}] = if_name;
-    ctx->eng.dirty = true;
+    ctx->eng.touch();
     return PG_OK;
 }
 int pg_set_host_interconnect_if_name(pg_ctx* ctx, const char* n) {
     if (!ctx) return PG_EINVAL;
     ctx->eng.ifaces.host_interconnect = sv(n);
-    ctx->eng.dirty = true;
+    ctx->eng.touch();
     return PG_OK;
 }
 int pg_set_main_interface_name(pg_ctx* ctx, const char* n) {
     if (!ctx) return PG_EINVAL;
     ctx->eng.ifaces.main_if = sv(n);
-    ctx->eng.dirty = true;
+    ctx->eng.touch();
     return PG_OK;
 }
 int pg_set_other_vpp_interfaces(pg_ctx* ctx, const char* const* names, size_t n) {
     if (!ctx) return PG_EINVAL;
     ctx->eng.ifaces.other_ifs.clear();
     for (size_t i = 0; i < n; i++) ctx->eng.ifaces.other_ifs.push_back(sv(names[i]));
-    ctx->eng.dirty = true;
+    ctx->eng.touch();
     return PG_OK;
 }
 int pg_set_vxlan_bvi_if_name(pg_ctx* ctx, const char* n) {
     if (!ctx) return PG_EINVAL;
     ctx->eng.ifaces.vxlan_bvi = sv(n);
-    ctx->eng.dirty = true;
+    ctx->eng.touch();
     return PG_OK;
 }
 int pg_register_pod(pg_ctx* ctx, const char* ns, const char* name, const char* ip, int another_node) {
@@ -169,7 +170,7 @@ int pg_register_pod(pg_ctx* ctx, const char* ns, const char* name, const char* i
     parse_ip(ip, &reg.ip);  // net.ParseIP; nil on failure like the reference
     reg.another_node = another_node != 0;
     ctx->eng.pods[PodID{ns, name}] = reg;
-    ctx->eng.dirty = true;
+    ctx->eng.touch();
     return PG_OK;
 }
 
@@ -373,6 +374,63 @@ int pg_table_info(pg_ctx* ctx, int table_id, uint32_t* rule_base, uint32_t* n_ru
     if (n_rules) *n_rules = (uint32_t)ctx->eng.by_name[ctx->eng.table_names[table_id]]->rules.size();
     if (default_slot) *default_slot = T.n_rules + (uint32_t)table_id;
     return PG_OK;
+}
+
+int pg_table_stats(pg_ctx* ctx, int table_id, uint32_t* flags, uint32_t* blob_bytes, uint32_t* n_src_classes,
+                   uint32_t* n_key_classes) {
+    if (!ctx) return PG_EINVAL;
+    GUARD_BEGIN
+    Engine& E = ctx->eng;
+    if (!E.compiled) E.compile();
+    if (table_id < 0 || (size_t)table_id >= E.host.tabs.size()) return fail(ctx, PG_EINVAL, "table id out of range");
+    const DevTable& hd = E.host.tabs[table_id];
+    const uint32_t* b = E.host.blobs.data() + hd.blob_off;
+    if (flags) *flags = hd.flags;
+    if (blob_bytes) *blob_bytes = hd.blob_words * 4;
+    if (n_src_classes) *n_src_classes = hd.blob_words ? b[10] : 0;
+    if (n_key_classes) *n_key_classes = (hd.blob_words && (hd.flags & kFlagCross)) ? b[7] : 0;
+    return PG_OK;
+    GUARD_END(ctx)
+}
+
+int pg_debug_walk_blob(pg_ctx* ctx, const char* acl_name, const uint32_t* src, const uint32_t* dst,
+                       const uint16_t* dst_port, const uint8_t* proto, uint64_t n, uint32_t* out) {
+    if (!ctx || !acl_name || (n && (!src || !dst || !dst_port || !proto || !out))) return PG_EINVAL;
+    GUARD_BEGIN
+    Engine& E = ctx->eng;
+    if (!E.compiled) E.compile();
+    auto it = E.table_of_acl.find(acl_name);
+    if (it == E.table_of_acl.end()) return fail(ctx, PG_ENOENT, "no such ACL");
+    const DevTable& hd = E.host.tabs[it->second];
+    const uint32_t NR = (uint32_t)E.host.rules.size();
+    HostLoader ld{E.host.blobs.data() + hd.blob_off};
+    BlobHdr bh{};
+    if (!(hd.flags & kFlagLinear)) bh = blob_hdr(ld);
+    for (uint64_t i = 0; i < n; i++) {
+        uint32_t key = pkt_key_host(proto[i], dst_port[i]);
+        if (proto[i] > 2) key = kKeyANY;
+        if (!(hd.flags & kFlagLinear) && key < kKeyANY) {
+            out[i] = blob_eval(ld, bh, src[i], dst[i], key);
+            continue;
+        }
+        uint32_t w = (kActDeny << 30) | (NR + (uint32_t)it->second);  // mirror of eval_linear_lane
+        for (uint32_t r = 0; r < hd.n_rules; r++) {
+            const DevRule& R = E.host.rules[hd.rule_base + r];
+            if ((src[i] & R.smask) != R.snet || (dst[i] & R.dmask) != R.dnet) continue;
+            if (key >= kKeyANY) {
+                if ((R.act >> 4) == kActNever) continue;
+                w = (((R.act >> 4) & 3u) << 30) | (hd.rule_base + r);
+                break;
+            }
+            if (key >= R.klo && key <= R.khi) {
+                w = ((R.act & 3u) << 30) | (hd.rule_base + r);
+                break;
+            }
+        }
+        out[i] = w;
+    }
+    return PG_OK;
+    GUARD_END(ctx)
 }
 
 int pg_classify(pg_ctx* ctx, int mode, int table_id, const pg_tuple_soa* t, uint64_t n, uint32_t* out,

@@ -19,6 +19,7 @@
 #include <algorithm>
 #include <cstring>
 
+#include "blobwalk.hpp"
 #include "device.hpp"
 
 namespace pg {
@@ -35,6 +36,7 @@ namespace pg {
 struct DeviceBuffers {
     void* blob = nullptr;
     DevTableSet view{};
+    std::vector<DevTable> host_tabs;
 };
 
 const DevTableSet& dev_view(const DeviceBuffers* b) { return b->view; }
@@ -83,11 +85,7 @@ DeviceBuffers* dev_upload(const HostTableSet& h, std::string* err) {
     };
     size_t o_rules = place(h.rules.size() * sizeof(DevRule));
     size_t o_tabs = place(h.tabs.size() * sizeof(DevTable));
-    size_t o_bnd = place(h.bnd.size() * 4);
-    size_t o_ivl = place(h.ivl.size() * 4);
-    size_t o_radix = place(h.radix.size() * 4);
-    size_t o_cand = place(h.cand.size() * 4);
-    size_t o_cr = place(h.cand_rule.size() * 4);
+    size_t o_blob = place(h.blobs.size() * 4);
     size_t o_if = place(h.ifaces.size() * 4);
     size_t o_ip = place(h.iphash.size() * 4);
     std::vector<uint8_t> img(off, 0);
@@ -96,11 +94,7 @@ DeviceBuffers* dev_upload(const HostTableSet& h, std::string* err) {
     };
     put(o_rules, h.rules.data(), h.rules.size() * sizeof(DevRule));
     put(o_tabs, h.tabs.data(), h.tabs.size() * sizeof(DevTable));
-    put(o_bnd, h.bnd.data(), h.bnd.size() * 4);
-    put(o_ivl, h.ivl.data(), h.ivl.size() * 4);
-    put(o_radix, h.radix.data(), h.radix.size() * 4);
-    put(o_cand, h.cand.data(), h.cand.size() * 4);
-    put(o_cr, h.cand_rule.data(), h.cand_rule.size() * 4);
+    put(o_blob, h.blobs.data(), h.blobs.size() * 4);
     put(o_if, h.ifaces.data(), h.ifaces.size() * 4);
     put(o_ip, h.iphash.data(), h.iphash.size() * 4);
     auto* b = new DeviceBuffers();
@@ -118,11 +112,7 @@ DeviceBuffers* dev_upload(const HostTableSet& h, std::string* err) {
     DevTableSet& v = b->view;
     v.rules = (const DevRule*)(base + o_rules);
     v.tabs = (const DevTable*)(base + o_tabs);
-    v.bnd = (const uint32_t*)(base + o_bnd);
-    v.ivl = (const uint32_t*)(base + o_ivl);
-    v.radix = (const uint32_t*)(base + o_radix);
-    v.cand = (const uint32_t*)(base + o_cand);
-    v.cand_rule = (const uint32_t*)(base + o_cr);
+    v.blobs = (const uint32_t*)(base + o_blob);
     v.ifaces = (const int32_t*)(base + o_if);
     v.iphash = (const uint32_t*)(base + o_ip);
     v.iphash_mask = h.iphash_mask;
@@ -133,6 +123,8 @@ DeviceBuffers* dev_upload(const HostTableSet& h, std::string* err) {
     v.slot_noacl = v.n_rules + v.n_tables;
     v.slot_unresolved = v.slot_noacl + 1;
     v.n_slots = v.slot_unresolved + 1;
+    b->host_tabs = h.tabs;
+    v.host_tabs = b->host_tabs.data();
     return b;
 }
 
@@ -169,29 +161,33 @@ __device__ __noinline__ uint32_t eval_linear_lane(const DevTableSet& T, uint32_t
     return verdict(kActDeny, T.n_rules + t);
 }
 
+// ---- classification blob walk (layout: fastpath.cpp, walk: blobwalk.hpp) -----------------------
+struct DevLoader {  // 16/8-byte loads; LDS or global depending on where the pointer came from
+    const uint32_t* b;
+    __device__ __forceinline__ uint32_t u32(uint32_t i) const { return b[i]; }
+    __device__ __forceinline__ W2 u2(uint32_t i) const {
+        const uint2 v = *reinterpret_cast<const uint2*>(b + i);
+        return W2{v.x, v.y};
+    }
+    __device__ __forceinline__ W4 u4(uint32_t i) const {
+        const uint4 v = *reinterpret_cast<const uint4*>(b + i);
+        return W4{v.x, v.y, v.z, v.w};
+    }
+};
+__device__ __forceinline__ BlobHdr load_hdr(const uint32_t* b) { return blob_hdr(DevLoader{b}); }
+__device__ __forceinline__ uint32_t eval_blob(const uint32_t* b, const BlobHdr& h, uint32_t src, uint32_t dst,
+                                              uint32_t key) {
+    return blob_eval(DevLoader{b}, h, src, dst, key);
+}
+
 // evalACL(table t) -- t < 0: no ACL on the interface (PERMIT, aclengine_mock.go:506-508)
 __device__ __forceinline__ uint32_t eval_table(const DevTableSet& T, int32_t t, uint32_t src, uint32_t dst,
                                                uint32_t key) {
     if (t < 0) return verdict(kActPermit, T.slot_noacl);
     const DevTable hd = T.tabs[t];
-    if ((hd.flags & 1u) || key >= kKeyANY) return eval_linear_lane(T, (uint32_t)t, src, dst, key);
-    const uint32_t x = hd.radix_shift >= 32u ? 0u : (src >> hd.radix_shift);
-    uint32_t lo = T.radix[hd.radix_base + x];
-    uint32_t hi = T.radix[hd.radix_base + x + 1];
-    const uint32_t* bnd = T.bnd + hd.bnd_base;
-    while (lo < hi) {
-        const uint32_t mid = (lo + hi + 1u) >> 1;
-        if (bnd[mid] <= src) lo = mid;
-        else hi = mid - 1u;
-    }
-    const uint2 iv = reinterpret_cast<const uint2*>(T.ivl)[hd.bnd_base + lo];
-    const uint4* c = reinterpret_cast<const uint4*>(T.cand) + iv.x;
-    for (uint32_t j = 0; j < iv.y; j++) {
-        const uint4 e = c[j];
-        if ((dst & e.y) == e.x && key >= (e.z & 0xFFFFFFu) && key <= e.w)
-            return verdict((e.z >> 24) & 3u, hd.rule_base + T.cand_rule[iv.x + j]);
-    }
-    return verdict(kActDeny, T.n_rules + (uint32_t)t);
+    if ((hd.flags & kFlagLinear) || key >= kKeyANY) return eval_linear_lane(T, (uint32_t)t, src, dst, key);
+    const uint32_t* b = T.blobs + hd.blob_off;
+    return eval_blob(b, load_hdr(b), src, dst, key);
 }
 
 __device__ __forceinline__ uint32_t hash_ip(uint32_t ip) {
@@ -272,11 +268,21 @@ __device__ __forceinline__ uint32_t test_connection(const DevTableSet& T, int32_
     return verdict(2u, w & 0x3FFFFFFFu);
 }
 
+// SINGLE mode: the table's blob (staged in LDS or read from HBM/L2) and its header
+struct Single {
+    const uint32_t* b;
+    BlobHdr hdr;
+    bool linear;
+};
+
 template <int MODE, bool COUNT>
-__device__ __forceinline__ uint32_t classify_one(const DevTableSet& T, int32_t t, uint32_t src, uint32_t dst,
-                                                 uint32_t sport, uint32_t dport, uint32_t proto, const Hist& h) {
+__device__ __forceinline__ uint32_t classify_one(const DevTableSet& T, int32_t t, const Single& sg, uint32_t src,
+                                                 uint32_t dst, uint32_t sport, uint32_t dport, uint32_t proto,
+                                                 const Hist& h) {
     if (MODE == 0) {  // SINGLE
-        const uint32_t w = eval_table(T, t, src, dst, pkt_key(proto, dport));
+        const uint32_t key = pkt_key(proto, dport);
+        const uint32_t w = (sg.linear || key >= kKeyANY) ? eval_linear_lane(T, (uint32_t)t, src, dst, key)
+                                                         : eval_blob(sg.b, sg.hdr, src, dst, key);
         if (COUNT) h.inc(w & 0x3FFFFFFFu);
         return w;
     } else if (MODE == 1) {  // PERPOD: outbound ACL of the egress interface of dst
@@ -298,21 +304,38 @@ __device__ __forceinline__ uint32_t classify_one(const DevTableSet& T, int32_t t
 constexpr int kBlock = 256;
 constexpr uint32_t kLdsHistMax = 16384;  // slots kept in LDS (64 KiB)
 
-template <int MODE, bool COUNT, bool VEC>
+// STAGE (SINGLE mode only): the table's blob (stage_words u32, multiple of 4) is copied into
+// LDS once per workgroup and every lookup of the grid-stride loop reads it from there.
+template <int MODE, bool COUNT, bool VEC, bool STAGE>
 __global__ __launch_bounds__(kBlock) void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
                                                      const uint32_t* __restrict__ dst,
                                                      const uint16_t* __restrict__ sport,
                                                      const uint16_t* __restrict__ dport,
                                                      const uint8_t* __restrict__ proto, uint64_t n,
-                                                     uint32_t* __restrict__ out, unsigned long long* counters) {
-    extern __shared__ uint32_t hist[];
+                                                     uint32_t* __restrict__ out, unsigned long long* counters,
+                                                     uint32_t stage_words) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+    uint32_t* hist = smem + (STAGE ? stage_words : 0u);
     Hist h{nullptr, counters};
     const bool use_lds = COUNT && T.n_slots <= kLdsHistMax;
+    Single sg{nullptr, BlobHdr{}, true};
+    if (MODE == 0) {
+        const DevTable hd = T.tabs[t];
+        sg.linear = (hd.flags & kFlagLinear) != 0u;
+        if (STAGE) {
+            const uint4* g = reinterpret_cast<const uint4*>(T.blobs + hd.blob_off);
+            for (uint32_t i = threadIdx.x; i < stage_words / 4u; i += kBlock) reinterpret_cast<uint4*>(smem)[i] = g[i];
+            sg.b = smem;
+        } else {
+            sg.b = T.blobs + hd.blob_off;
+        }
+    }
     if (COUNT && use_lds) {
         for (uint32_t i = threadIdx.x; i < T.n_slots; i += kBlock) hist[i] = 0;
-        __syncthreads();
         h.lds = hist;
     }
+    if (STAGE || (COUNT && use_lds)) __syncthreads();
+    if (MODE == 0 && !sg.linear) sg.hdr = load_hdr(sg.b);
     const uint64_t nq = (n + 3) >> 2;
     const uint64_t stride = (uint64_t)gridDim.x * kBlock;
     for (uint64_t q = (uint64_t)blockIdx.x * kBlock + threadIdx.x; q < nq; q += stride) {
@@ -325,14 +348,15 @@ __global__ __launch_bounds__(kBlock) void k_classify(DevTableSet T, int32_t t, c
             uint2 sp = make_uint2(0, 0);
             if (MODE == 2) sp = *reinterpret_cast<const uint2*>(sport + i0);
             uint4 o;
-            o.x = classify_one<MODE, COUNT>(T, t, s.x, d.x, sp.x & 0xFFFFu, dp.x & 0xFFFFu, pr & 0xFFu, h);
-            o.y = classify_one<MODE, COUNT>(T, t, s.y, d.y, sp.x >> 16, dp.x >> 16, (pr >> 8) & 0xFFu, h);
-            o.z = classify_one<MODE, COUNT>(T, t, s.z, d.z, sp.y & 0xFFFFu, dp.y & 0xFFFFu, (pr >> 16) & 0xFFu, h);
-            o.w = classify_one<MODE, COUNT>(T, t, s.w, d.w, sp.y >> 16, dp.y >> 16, pr >> 24, h);
+            o.x = classify_one<MODE, COUNT>(T, t, sg, s.x, d.x, sp.x & 0xFFFFu, dp.x & 0xFFFFu, pr & 0xFFu, h);
+            o.y = classify_one<MODE, COUNT>(T, t, sg, s.y, d.y, sp.x >> 16, dp.x >> 16, (pr >> 8) & 0xFFu, h);
+            o.z = classify_one<MODE, COUNT>(T, t, sg, s.z, d.z, sp.y & 0xFFFFu, dp.y & 0xFFFFu, (pr >> 16) & 0xFFu,
+                                            h);
+            o.w = classify_one<MODE, COUNT>(T, t, sg, s.w, d.w, sp.y >> 16, dp.y >> 16, pr >> 24, h);
             *reinterpret_cast<uint4*>(out + i0) = o;
         } else {
             for (uint64_t i = i0; i < n && i < i0 + 4; i++)
-                out[i] = classify_one<MODE, COUNT>(T, t, src[i], dst[i], MODE == 2 ? sport[i] : 0u, dport[i],
+                out[i] = classify_one<MODE, COUNT>(T, t, sg, src[i], dst[i], MODE == 2 ? sport[i] : 0u, dport[i],
                                                    proto[i], h);
         }
     }
@@ -465,13 +489,25 @@ static int grid_for(uint64_t items) {
     return (int)std::max<uint64_t>(1, std::min<uint64_t>(g, 256ull * 8ull));
 }
 
+constexpr uint32_t kStageMaxWords = 16384;  // blobs up to 64 KiB are staged in LDS
+
 template <int MODE, bool COUNT, bool VEC>
 static void launch_classify(const DevTableSet& T, int t, const uint32_t* src, const uint32_t* dst,
                             const uint16_t* sport, const uint16_t* dport, const uint8_t* proto, uint64_t n,
                             uint32_t* out, unsigned long long* counters, hipStream_t st) {
-    const size_t lds = (COUNT && T.n_slots <= kLdsHistMax) ? T.n_slots * 4 : 0;
-    hipLaunchKernelGGL((k_classify<MODE, COUNT, VEC>), dim3(grid_for((n + 3) / 4)), dim3(kBlock), lds, st, T, t, src,
-                       dst, sport, dport, proto, n, out, counters);
+    const size_t hist = (COUNT && T.n_slots <= kLdsHistMax) ? T.n_slots * 4 : 0;
+    uint32_t stage = 0;
+    if (MODE == 0) {
+        const DevTable& hd = T.host_tabs[t];
+        if (!(hd.flags & kFlagLinear) && hd.blob_words <= kStageMaxWords) stage = hd.blob_words;
+    }
+    const dim3 grid(grid_for((n + 3) / 4));
+    if (stage)
+        hipLaunchKernelGGL((k_classify<MODE, COUNT, VEC, true>), grid, dim3(kBlock), hist + stage * 4, st, T, t, src,
+                           dst, sport, dport, proto, n, out, counters, stage);
+    else
+        hipLaunchKernelGGL((k_classify<MODE, COUNT, VEC, false>), grid, dim3(kBlock), hist, st, T, t, src, dst, sport,
+                           dport, proto, n, out, counters, 0u);
 }
 
 template <int MODE>

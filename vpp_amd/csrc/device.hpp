@@ -1,16 +1,13 @@
-// Device-side data layout shared by the host compiler (engine.cpp) and the HIP kernels
-// (device.hip). Everything here is plain-old-data copied to HBM as flat arrays.
+// Device-side data layout shared by the host compiler (engine.cpp, fastpath.cpp) and the
+// HIP kernels (device.hip). Everything here is plain-old-data copied to HBM as flat arrays.
 //
-// Layout in HBM (one "table set", double-buffered by the engine):
-//   rules    DevRule[NR]        all ACLs' rules, concatenated, ACL order preserved
-//   tabs     DevTable[T]        per-ACL header
-//   bnd      u32[]              per table: sorted start addresses of its src intervals
-//   ivl      uint2[]            per interval: {first candidate, candidate count}
-//   radix    u32[]              per table: 2^bits+1 entries, interval of (x << (32-bits))
-//   cand     uint4[]            per interval candidate list: {dnet, dmask, klo|act<<24, khi}
-//   cand_rule u32[]             rule index (in its ACL) of each candidate
-//   ifaces   int2[NI]           per interface {inbound table, outbound table} (-1 = no ACL)
-//   iphash   uint2[cap]         IPv4 -> interface (open addressing, EMPTY = 0xFFFFFFFF value)
+// Layout in HBM (one "table set"; a new set is uploaded and swapped in on every change):
+//   rules   DevRule[NR]   all ACLs' rules concatenated, ACL order preserved (linear kernel,
+//                         ANY-protocol packets, generator)
+//   tabs    DevTable[T]   per-ACL header
+//   blobs   u32[]         per-ACL classification blob (fastpath.cpp), 16-byte aligned
+//   ifaces  int2[NI]      per interface {inbound table, outbound table} (-1 = no ACL)
+//   iphash  uint2[cap]    IPv4 -> interface (open addressing, EMPTY = 0xFFFFFFFF value)
 #pragma once
 #include <cstdint>
 #include <string>
@@ -34,22 +31,16 @@ struct DevRule {           // 32 B, one compiled vpp_acl rule
 struct DevTable {          // 32 B
     uint32_t rule_base;    // first rule (global index == counter slot)
     uint32_t n_rules;
-    uint32_t bnd_base;     // first interval (into bnd / ivl)
-    uint32_t nb;           // intervals (>= 1)
-    uint32_t radix_base;
-    uint32_t radix_shift;  // 32 - bits
-    uint32_t flags;
-    uint32_t pad;
+    uint32_t blob_off;     // in u32 words, multiple of 4
+    uint32_t blob_words;
+    uint32_t flags;        // copy of blob[0]
+    uint32_t pad[3];
 };
 
 struct DevTableSet {       // device pointers (valid on the GPU)
     const DevRule* rules;
     const DevTable* tabs;
-    const uint32_t* bnd;
-    const uint32_t* ivl;   // uint2 pairs
-    const uint32_t* radix;
-    const uint32_t* cand;  // uint4 quads
-    const uint32_t* cand_rule;
+    const uint32_t* blobs;
     const int32_t* ifaces; // int2 pairs
     const uint32_t* iphash;// uint2 pairs {ip, iface}
     uint32_t iphash_mask;
@@ -60,18 +51,23 @@ struct DevTableSet {       // device pointers (valid on the GPU)
     uint32_t slot_noacl;   // NR + T
     uint32_t slot_unresolved;
     uint32_t n_slots;
+    const DevTable* host_tabs;  // host copy of tabs (launch decisions; not dereferenced on the GPU)
 };
 
 // Host image of a table set, produced by the compiler and uploaded as one blob.
 struct HostTableSet {
     std::vector<DevRule> rules;
     std::vector<DevTable> tabs;
-    std::vector<uint32_t> bnd, ivl, radix, cand, cand_rule;
+    std::vector<uint32_t> blobs;
     std::vector<int32_t> ifaces;
     std::vector<uint32_t> iphash;
     uint32_t iphash_mask = 0;
     int32_t node_if = -1;
 };
+
+// fastpath.cpp: classification blob of one table (false = does not fit the budgets)
+bool build_fast_table(const DevRule* rules, uint32_t n, uint32_t rule_base, uint32_t default_slot,
+                      std::vector<uint32_t>& blob, uint64_t cross_budget);
 
 struct GenParams {         // device view of pg_gen_spec
     uint64_t seed, index_base;
@@ -80,7 +76,7 @@ struct GenParams {         // device view of pg_gen_spec
     uint32_t n_ip_pool, n_port_pool;
     const uint32_t* ip_pool;
     const uint16_t* port_pool;
-    const uint32_t* zipf_cdf;  // n_rules+1 entries or null
+    const uint32_t* zipf_cdf;  // n_rules entries or null
 };
 
 struct ConnQueryDev {      // resolved Connection* query
@@ -88,8 +84,7 @@ struct ConnQueryDev {      // resolved Connection* query
     int32_t src_if, dst_if;
     uint32_t key_syn;      // L4 key with dport
     uint32_t key_synack;   // L4 key with sport
-    uint32_t same_if;
-    uint32_t pad;
+    uint32_t pad[2];
 };
 
 // ---- device API (device.hip) ----------------------------------------------------------

@@ -77,90 +77,6 @@ DevRule compile_acl_rule(const AclRule& r) {
     return d;
 }
 
-static bool unconditional(const DevRule& r) {  // matches every packet that reaches it
-    return r.dmask == 0 && r.klo == 0 && r.khi == kKeyMax;
-}
-
-// ---- src-interval index ---------------------------------------------------------------
-// The IPv4 src space is cut at every rule's src-prefix boundary; inside one interval the
-// set of rules whose src matches is constant. Each interval keeps that set (ascending rule
-// index, truncated after the first rule that matches unconditionally), so the device only
-// tests dst + L4 of the candidates and the first hit is the first match of the ACL.
-bool build_table_index(const DevRule* rules, uint32_t n, HostTableSet& h, DevTable& hdr, uint64_t cand_budget) {
-    std::vector<uint32_t> bnd{0};
-    for (uint32_t i = 0; i < n; i++) {
-        const DevRule& r = rules[i];
-        if (r.smask == 0 || (r.klo > r.khi && (r.act >> 4) == kActNever)) continue;
-        bnd.push_back(r.snet);
-        uint64_t end = (uint64_t)r.snet + (uint64_t)(~r.smask) + 1ull;
-        if (end < (1ull << 32)) bnd.push_back((uint32_t)end);
-    }
-    std::sort(bnd.begin(), bnd.end());
-    bnd.erase(std::unique(bnd.begin(), bnd.end()), bnd.end());
-    uint32_t nb = (uint32_t)bnd.size();
-
-    // sweep: events per boundary (rules starting / ending there)
-    std::vector<std::pair<uint32_t, uint32_t>> starts, ends;  // (addr, rule)
-    std::set<uint32_t> active;                                // rule indices whose src covers the sweep point
-    for (uint32_t i = 0; i < n; i++) {
-        const DevRule& r = rules[i];
-        if (r.klo > r.khi && (r.act >> 4) == kActNever) continue;  // never matches
-        if (r.smask == 0) {
-            active.insert(i);
-            continue;
-        }
-        starts.push_back({r.snet, i});
-        uint64_t end = (uint64_t)r.snet + (uint64_t)(~r.smask) + 1ull;
-        if (end < (1ull << 32)) ends.push_back({(uint32_t)end, i});
-    }
-    std::sort(starts.begin(), starts.end());
-    std::sort(ends.begin(), ends.end());
-    size_t si = 0, ei = 0;
-    uint64_t total = 0;
-    hdr.bnd_base = (uint32_t)h.bnd.size();
-    hdr.nb = nb;
-    for (uint32_t k = 0; k < nb; k++) {
-        uint32_t a = bnd[k];
-        while (ei < ends.size() && ends[ei].first <= a) active.erase(ends[ei++].second);
-        while (si < starts.size() && starts[si].first <= a) active.insert(starts[si++].second);
-        h.bnd.push_back(a);
-        uint32_t first = (uint32_t)(h.cand_rule.size());
-        uint32_t cnt = 0;
-        for (uint32_t ri : active) {
-            const DevRule& r = rules[ri];
-            if (r.klo <= r.khi || (r.act >> 4) != kActNever) {
-                h.cand.push_back(r.dnet);
-                h.cand.push_back(r.dmask);
-                h.cand.push_back(r.klo | ((r.act & 0xFF) << 24));
-                h.cand.push_back(r.khi);
-                h.cand_rule.push_back(ri);
-                cnt++;
-            }
-            if (unconditional(r)) break;
-        }
-        h.ivl.push_back(first);
-        h.ivl.push_back(cnt);
-        total += cnt;
-        if (total > cand_budget) return false;
-    }
-    // radix over the top bits: interval containing (x << shift)
-    uint32_t bits = 0;
-    while ((1u << bits) < nb && bits < 16) bits++;
-    if (nb > 8 && bits < 16) bits++;
-    if (nb <= 8) bits = 0;
-    hdr.radix_base = (uint32_t)h.radix.size();
-    hdr.radix_shift = 32 - bits;
-    uint32_t nbuckets = 1u << bits;
-    uint32_t k = 0;
-    for (uint32_t x = 0; x < nbuckets; x++) {
-        uint64_t addr = bits ? ((uint64_t)x << (32 - bits)) : 0;
-        while (k + 1 < nb && bnd[k + 1] <= addr) k++;
-        h.radix.push_back(k);
-    }
-    h.radix.push_back(nb - 1);
-    return true;
-}
-
 // ---- Engine ------------------------------------------------------------------------------
 Engine::~Engine() {
     if (cur) dev_free(cur);
@@ -176,7 +92,7 @@ std::string Engine::del_acl(const std::string& name) {  // aclengine_mock.go:664
         if (kv.second.second && kv.second.second->name == name) kv.second.second = nullptr;
     }
     changes++;
-    dirty = true;
+    touch();
     return "";
 }
 
@@ -191,13 +107,13 @@ std::string Engine::put_acl(const ACLPtr& acl) {  // aclengine_mock.go:683-712
     for (auto& i : acl->ingress) by_if[i].first = acl;
     for (auto& i : acl->egress) by_if[i].second = acl;
     changes++;
-    dirty = true;
+    touch();
     return "";
 }
 
 std::string Engine::apply_txn(bool resync, const AclOps& ops) {  // aclengine_mock.go:151-228
     committed++;
-    dirty = true;
+    touch();
     if (resync) {
         by_name.clear();
         by_if.clear();
@@ -240,7 +156,40 @@ static uint32_t hash_ip(uint32_t ip) {
 
 int Engine::sync() {
     if (!dirty && cur) return PG_OK;
-    HostTableSet h;
+    if (!compiled) compile();
+    HostTableSet& h = host;
+    std::string err;
+    DeviceBuffers* nb = dev_upload(h, &err);
+    if (!nb) {
+        last_error = "upload: " + err;
+        return PG_EIO;
+    }
+    if (cur) dev_free(cur);  // dev_upload synchronises before returning: old set is idle
+    cur = nb;
+    size_t slots = dev_view(cur).n_slots;
+    if (slots != counter_slots) {
+        if (counters) dev_release(counters);
+        counters = (unsigned long long*)dev_alloc(slots * sizeof(unsigned long long), &err);
+        if (!counters) {
+            last_error = err;
+            counter_slots = 0;
+            return PG_ENOMEM;
+        }
+        counter_slots = slots;
+    }
+    // slot meanings change with the tables: counters restart from zero
+    if (dev_memset(counters, 0, slots * 8, nullptr, &err) != 0 || dev_sync(&err) != 0) {
+        last_error = err;
+        return PG_EIO;
+    }
+    dirty = false;
+    return PG_OK;
+}
+
+// ACLs -> host image of the device table set (rules, blobs, interface maps); no GPU needed.
+void Engine::compile() {
+    host = HostTableSet();
+    HostTableSet& h = host;
     table_of_acl.clear();
     table_names.clear();
     slot_table.clear();
@@ -259,14 +208,20 @@ int Engine::sync() {
         }
         h.tabs.push_back(hdr);
     }
-    const uint64_t budget = 1ull << 27;  // candidate entries (2 GiB at 16+4 B) before linear fallback
+    const uint32_t NR = (uint32_t)h.rules.size();
     for (size_t t = 0; t < h.tabs.size(); t++) {
         DevTable& hdr = h.tabs[t];
-        size_t b0 = h.bnd.size(), i0 = h.ivl.size(), r0 = h.radix.size(), c0 = h.cand.size(), cr0 = h.cand_rule.size();
-        if (!build_table_index(h.rules.data() + hdr.rule_base, hdr.n_rules, h, hdr, budget)) {
-            h.bnd.resize(b0), h.ivl.resize(i0), h.radix.resize(r0), h.cand.resize(c0), h.cand_rule.resize(cr0);
-            hdr.flags = 1;  // linear scan
-            hdr.nb = 0;
+        std::vector<uint32_t> blob;
+        hdr.blob_off = (uint32_t)h.blobs.size();
+        if (build_fast_table(h.rules.data() + hdr.rule_base, hdr.n_rules, hdr.rule_base, NR + (uint32_t)t, blob,
+                             1ull << 22)) {
+            while (blob.size() % 4) blob.push_back(0);
+            hdr.flags = blob[0];
+            hdr.blob_words = (uint32_t)blob.size();
+            h.blobs.insert(h.blobs.end(), blob.begin(), blob.end());
+        } else {
+            hdr.flags = 8;  // linear scan fallback
+            hdr.blob_words = 0;
         }
     }
     uint32_t T = (uint32_t)h.tabs.size();
@@ -309,33 +264,7 @@ int Engine::sync() {
         h.iphash[2 * s] = e.first;
         h.iphash[2 * s + 1] = (uint32_t)e.second;
     }
-
-    std::string err;
-    DeviceBuffers* nb = dev_upload(h, &err);
-    if (!nb) {
-        last_error = "upload: " + err;
-        return PG_EIO;
-    }
-    if (cur) dev_free(cur);  // dev_upload synchronises before returning: old set is idle
-    cur = nb;
-    size_t slots = dev_view(cur).n_slots;
-    if (slots != counter_slots) {
-        if (counters) dev_release(counters);
-        counters = (unsigned long long*)dev_alloc(slots * sizeof(unsigned long long), &err);
-        if (!counters) {
-            last_error = err;
-            counter_slots = 0;
-            return PG_ENOMEM;
-        }
-        counter_slots = slots;
-    }
-    // slot meanings change with the tables: counters restart from zero
-    if (dev_memset(counters, 0, slots * 8, nullptr, &err) != 0 || dev_sync(&err) != 0) {
-        last_error = err;
-        return PG_EIO;
-    }
-    dirty = false;
-    return PG_OK;
+    compiled = true;
 }
 
 }  // namespace pg

@@ -19,8 +19,6 @@ struct PodReg {
 
 // Compiled form of one vpp_acl rule (evalACL semantics, aclengine_mock.go:510-649).
 DevRule compile_acl_rule(const AclRule& r);
-// Src-interval candidate index of one table (appends to h, fills hdr).
-bool build_table_index(const DevRule* rules, uint32_t n, HostTableSet& h, DevTable& hdr, uint64_t cand_budget);
 
 struct Engine {
     int device = 0;
@@ -35,7 +33,9 @@ struct Engine {
     int committed = 0;
 
     // compiled / device state
-    bool dirty = true;
+    bool dirty = true;     // device tables stale
+    bool compiled = false; // `host` reflects the installed ACLs
+    HostTableSet host;
     DeviceBuffers* cur = nullptr;
     std::map<std::string, int> table_of_acl;
     std::vector<std::string> table_names;
@@ -48,7 +48,9 @@ struct Engine {
     std::string apply_txn(bool resync, const AclOps& ops);
     std::string put_acl(const ACLPtr& acl);
     std::string del_acl(const std::string& name);
-    int sync();  // compile + upload if dirty; returns PG_* code
+    int sync();      // compile + upload if dirty; returns PG_* code
+    void compile();  // host image only (no GPU)
+    void touch() { dirty = true, compiled = false; }
     const DevTableSet* view() const;
     int iface_of(const std::string& name) const;
     std::string node_if_name() const;

@@ -1,0 +1,293 @@
+// Builder of the per-table classification blob (the structure the K2 kernel walks).
+//
+// A table is the compiled first-match rule list of one ACL. The blob answers
+// evalACL(table, src, dst, key) for every TCP/UDP/OTHER packet with a bounded number of
+// dependent loads, independent of rule depth:
+//
+//   src  --multibit trie (root stride s1, then 8-bit strides; leaf-pushed)-->  src class
+//   key  --multibit trie over the 18-bit L4 key (root stride k1, then 8)----->  key class
+//   CROSS mode:  cross[src class][key class] -> verdict of the first rule whose src and L4
+//                match and whose dst is ANY, plus (LISTS) the short ordered list of
+//                dst-specific rules in front of it, tested on dst only.
+//   CAND mode:   (tables too large for a cross product) src class -> ordered candidate list
+//                of rules whose src matches, tested on dst + L4 key.
+//
+// src classes = equivalence classes of the elementary src intervals (cut at every rule's
+// prefix boundary) by the ordered list of rules whose src covers them, truncated after the
+// first rule that matches every packet reaching it. key classes = equivalence classes of
+// the elementary key segments by the set of rules whose key range covers them. The first
+// match of the ACL is the first rule of (src list) whose key range covers the key and whose
+// dst matches, which is exactly what the cross product precomputes (RFC, Gupta & McKeown,
+// SIGCOMM'99, specialised to first-match with a dst residue).
+//
+// Blob words (u32), all offsets relative to the blob start so it can be read from HBM or
+// copied verbatim into LDS:
+//   [0]  flags: 1 = CROSS, 2 = LISTS, 4 = CAND
+//   [1]  default verdict (DENY << 30 | table's default slot)
+//   [2]  src trie root   [3] s1     [4] key trie root   [5] k1
+//   [6]  cross / class-table offset [7] n_key_classes   [8] list / candidate offset
+//   [9]  candidate verdict offset   [10] n_src_classes  [11..15] reserved
+#include <algorithm>
+#include <map>
+#include <set>
+#include <unordered_map>
+
+#include "engine.hpp"
+
+namespace pg {
+
+namespace {
+
+constexpr uint32_t kLeaf = 0x80000000u;
+
+struct VecHash {
+    size_t operator()(const std::vector<uint32_t>& v) const {
+        uint64_t h = 1469598103934665603ull;
+        for (uint32_t x : v) {
+            h ^= x;
+            h *= 1099511628211ull;
+        }
+        return (size_t)h;
+    }
+};
+
+// Multibit trie over [0, 2^W): intervals given by sorted starts `bnd` (bnd[0] == 0) and a
+// class per interval. Appends blocks to `blob`; returns the root offset.
+uint32_t build_trie(std::vector<uint32_t>& blob, const std::vector<uint64_t>& bnd, const std::vector<uint32_t>& cls,
+                    uint32_t W, uint32_t s1) {
+    // interval index containing address a
+    auto find = [&](uint64_t a) { return (size_t)(std::upper_bound(bnd.begin(), bnd.end(), a) - bnd.begin()) - 1; };
+    struct Job {
+        uint32_t block;  // offset of the block in blob
+        uint64_t base;   // first address covered by the block
+        uint32_t shift;  // address bits below this level
+        uint32_t stride;
+    };
+    std::vector<Job> stack;
+    uint32_t root = (uint32_t)blob.size();
+    blob.resize(blob.size() + (1u << s1), 0);
+    stack.push_back({root, 0, W - s1, s1});
+    while (!stack.empty()) {
+        Job j = stack.back();
+        stack.pop_back();
+        uint64_t span = 1ull << j.shift;
+        for (uint32_t e = 0; e < (1u << j.stride); e++) {
+            uint64_t a = j.base + (uint64_t)e * span;
+            if (a >= (1ull << W)) {  // beyond the key space: unreachable, point at class 0
+                blob[j.block + e] = kLeaf | cls[0];
+                continue;
+            }
+            size_t k = find(a);
+            bool split = k + 1 < bnd.size() && bnd[k + 1] < a + span;
+            if (!split || j.shift == 0) {
+                blob[j.block + e] = kLeaf | cls[k];
+                continue;
+            }
+            uint32_t st = std::min<uint32_t>(8, j.shift);
+            uint32_t child = (uint32_t)blob.size();
+            blob.resize(blob.size() + (1u << st), 0);
+            blob[j.block + e] = child;
+            stack.push_back({child, a, j.shift - st, st});
+        }
+    }
+    return root;
+}
+
+uint32_t pick_stride(size_t nb, uint32_t W) {
+    uint32_t s = 4;
+    while (s < 16 && s < W && (1ull << s) < 4 * (uint64_t)nb) s += 4;
+    return std::min(s, W);
+}
+
+bool unconditional(const DevRule& r) { return r.dmask == 0 && r.klo == 0 && r.khi == kKeyMax; }
+bool live(const DevRule& r) { return r.klo <= r.khi; }  // can match a TCP/UDP/OTHER packet
+
+}  // namespace
+
+bool build_fast_table(const DevRule* rules, uint32_t n, uint32_t rule_base, uint32_t default_slot,
+                      std::vector<uint32_t>& blob, uint64_t cross_budget) {
+    blob.assign(16, 0);
+    const uint32_t dflt = (kActDeny << 30) | default_slot;
+    blob[1] = dflt;
+    auto verdict = [&](uint32_t i) { return ((rules[i].act & 3u) << 30) | (rule_base + i); };
+
+    // ---- src: elementary intervals and their candidate lists ------------------------------
+    std::vector<uint64_t> sb{0};
+    for (uint32_t i = 0; i < n; i++) {
+        const DevRule& r = rules[i];
+        if (r.smask == 0 || !live(r)) continue;
+        sb.push_back(r.snet);
+        uint64_t end = (uint64_t)r.snet + (uint64_t)(~r.smask) + 1ull;
+        if (end < (1ull << 32)) sb.push_back(end);
+    }
+    std::sort(sb.begin(), sb.end());
+    sb.erase(std::unique(sb.begin(), sb.end()), sb.end());
+    std::vector<std::pair<uint64_t, uint32_t>> starts, ends;
+    std::set<uint32_t> active;
+    for (uint32_t i = 0; i < n; i++) {
+        const DevRule& r = rules[i];
+        if (!live(r)) continue;
+        if (r.smask == 0) {
+            active.insert(i);
+            continue;
+        }
+        starts.push_back({r.snet, i});
+        uint64_t end = (uint64_t)r.snet + (uint64_t)(~r.smask) + 1ull;
+        if (end < (1ull << 32)) ends.push_back({end, i});
+    }
+    std::sort(starts.begin(), starts.end());
+    std::sort(ends.begin(), ends.end());
+    std::unordered_map<std::vector<uint32_t>, uint32_t, VecHash> src_cls_of;
+    std::vector<std::vector<uint32_t>> src_lists;
+    std::vector<uint32_t> sint_cls(sb.size());
+    size_t si = 0, ei = 0;
+    uint64_t total_cand = 0;
+    for (size_t k = 0; k < sb.size(); k++) {
+        while (ei < ends.size() && ends[ei].first <= sb[k]) active.erase(ends[ei++].second);
+        while (si < starts.size() && starts[si].first <= sb[k]) active.insert(starts[si++].second);
+        std::vector<uint32_t> lst;
+        for (uint32_t ri : active) {
+            lst.push_back(ri);
+            if (unconditional(rules[ri])) break;
+        }
+        auto it = src_cls_of.find(lst);
+        if (it == src_cls_of.end()) {
+            it = src_cls_of.emplace(lst, (uint32_t)src_lists.size()).first;
+            total_cand += lst.size();
+            src_lists.push_back(lst);
+            if (total_cand > (1ull << 26)) return false;
+        }
+        sint_cls[k] = it->second;
+    }
+    const uint32_t nsc = (uint32_t)src_lists.size();
+    uint32_t s1 = pick_stride(sb.size(), 32);
+    blob[2] = build_trie(blob, sb, sint_cls, 32, s1);
+    blob[3] = s1;
+    blob[10] = nsc;
+
+    // ---- try the cross product ---------------------------------------------------------
+    bool cross = n <= 16384;
+    std::vector<uint64_t> kb{0};
+    std::vector<uint32_t> kseg_cls;
+    std::vector<std::vector<uint32_t>> key_sets;  // sorted rule indices covering the segment
+    if (cross) {
+        for (uint32_t i = 0; i < n; i++) {
+            if (!live(rules[i])) continue;
+            kb.push_back(rules[i].klo);
+            if ((uint64_t)rules[i].khi + 1 <= kKeyMax) kb.push_back((uint64_t)rules[i].khi + 1);
+        }
+        std::sort(kb.begin(), kb.end());
+        kb.erase(std::unique(kb.begin(), kb.end()), kb.end());
+        std::vector<std::pair<uint64_t, uint32_t>> ks, ke;
+        for (uint32_t i = 0; i < n; i++) {
+            if (!live(rules[i])) continue;
+            ks.push_back({rules[i].klo, i});
+            if ((uint64_t)rules[i].khi + 1 <= kKeyMax) ke.push_back({(uint64_t)rules[i].khi + 1, i});
+        }
+        std::sort(ks.begin(), ks.end());
+        std::sort(ke.begin(), ke.end());
+        std::set<uint32_t> kact;
+        std::unordered_map<std::vector<uint32_t>, uint32_t, VecHash> key_cls_of;
+        size_t a = 0, b = 0;
+        kseg_cls.resize(kb.size());
+        for (size_t k = 0; k < kb.size(); k++) {
+            while (b < ke.size() && ke[b].first <= kb[k]) kact.erase(ke[b++].second);
+            while (a < ks.size() && ks[a].first <= kb[k]) kact.insert(ks[a++].second);
+            std::vector<uint32_t> v(kact.begin(), kact.end());
+            auto it = key_cls_of.find(v);
+            if (it == key_cls_of.end()) {
+                it = key_cls_of.emplace(v, (uint32_t)key_sets.size()).first;
+                key_sets.push_back(std::move(v));
+            }
+            kseg_cls[k] = it->second;
+        }
+        if ((uint64_t)nsc * key_sets.size() > cross_budget) cross = false;
+    }
+
+    if (cross) {
+        const uint32_t nkc = (uint32_t)key_sets.size();
+        uint32_t k1 = pick_stride(kb.size(), 18);
+        blob[4] = build_trie(blob, kb, kseg_cls, 18, k1);
+        blob[5] = k1;
+        blob[7] = nkc;
+        // membership bitsets of key classes
+        const size_t words = (n + 63) / 64;
+        std::vector<uint64_t> kbits((size_t)nkc * words, 0);
+        for (uint32_t c = 0; c < nkc; c++)
+            for (uint32_t r : key_sets[c]) kbits[(size_t)c * words + r / 64] |= 1ull << (r % 64);
+        std::vector<uint32_t> cverd((size_t)nsc * nkc);
+        std::vector<std::vector<uint32_t>> clist((size_t)nsc * nkc);
+        bool lists = false;
+        for (uint32_t s = 0; s < nsc; s++) {
+            for (uint32_t c = 0; c < nkc; c++) {
+                const uint64_t* bits = &kbits[(size_t)c * words];
+                uint32_t v = dflt;
+                std::vector<uint32_t>& L = clist[(size_t)s * nkc + c];
+                for (uint32_t r : src_lists[s]) {
+                    if (!((bits[r / 64] >> (r % 64)) & 1)) continue;
+                    if (rules[r].dmask == 0) {
+                        v = verdict(r);
+                        break;
+                    }
+                    L.push_back(r);
+                }
+                if (L.size() > 255) return build_fast_table(rules, n, rule_base, default_slot, blob, 0);
+                if (!L.empty()) lists = true;
+                cverd[(size_t)s * nkc + c] = v;
+            }
+        }
+        while (blob.size() % 4) blob.push_back(0);
+        blob[6] = (uint32_t)blob.size();
+        if (!lists) {
+            blob[0] = 1;
+            blob.insert(blob.end(), cverd.begin(), cverd.end());
+        } else {
+            blob[0] = 1 | 2;
+            size_t xoff = blob.size();
+            blob.resize(blob.size() + 2 * cverd.size(), 0);
+            for (size_t e = 0; e < cverd.size(); e++) {
+                blob[xoff + 2 * e] = cverd[e];
+                const auto& L = clist[e];
+                if (L.empty()) continue;
+                while (blob.size() % 4) blob.push_back(0);
+                uint32_t loff = (uint32_t)blob.size();
+                if (loff >= (1u << 24)) return build_fast_table(rules, n, rule_base, default_slot, blob, 0);
+                for (uint32_t r : L) {
+                    blob.push_back(rules[r].dnet);
+                    blob.push_back(rules[r].dmask);
+                    blob.push_back(verdict(r));
+                    blob.push_back(0);
+                }
+                blob[xoff + 2 * e + 1] = (loff << 8) | (uint32_t)L.size();
+            }
+        }
+        return true;
+    }
+
+    // ---- candidate mode -------------------------------------------------------------------
+    blob[0] = 4;
+    while (blob.size() % 4) blob.push_back(0);
+    blob[6] = (uint32_t)blob.size();  // per src class {cand offset (in entries), count}
+    size_t coff = blob.size();
+    blob.resize(blob.size() + 2 * (size_t)nsc, 0);
+    std::vector<uint32_t> cand, cverd;
+    for (uint32_t s = 0; s < nsc; s++) {
+        blob[coff + 2 * s] = (uint32_t)(cverd.size());
+        blob[coff + 2 * s + 1] = (uint32_t)src_lists[s].size();
+        for (uint32_t r : src_lists[s]) {
+            cand.push_back(rules[r].dnet);
+            cand.push_back(rules[r].dmask);
+            cand.push_back(rules[r].klo);
+            cand.push_back(rules[r].khi);
+            cverd.push_back(verdict(r));
+        }
+    }
+    while (blob.size() % 4) blob.push_back(0);  // uint4 alignment of the candidate array
+    blob[8] = (uint32_t)blob.size();
+    blob.insert(blob.end(), cand.begin(), cand.end());
+    blob[9] = (uint32_t)blob.size();
+    blob.insert(blob.end(), cverd.begin(), cverd.end());
+    return true;
+}
+
+}  // namespace pg

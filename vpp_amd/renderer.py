@@ -235,6 +235,24 @@ class Engine:
         self._ck(lib.pg_table_info(self.h, tid, C.byref(b), C.byref(n), C.byref(d)))
         return b.value, n.value, d.value
 
+    def table_stats(self, tid):
+        v = [C.c_uint32() for _ in range(4)]
+        self._ck(lib.pg_table_stats(self.h, tid, *[C.byref(x) for x in v]))
+        f, nbytes, nsc, nkc = (x.value for x in v)
+        mode = "linear" if f & 8 else ("cand" if f & 4 else ("cross+lists" if f & 2 else "cross"))
+        return {"structure": mode, "blob_bytes": nbytes, "src_classes": nsc, "key_classes": nkc}
+
+    def debug_walk(self, acl_name, src, dst, dport, proto):
+        """TESTS ONLY: host walk of the ACL's compiled blob (see pg_debug_walk_blob)."""
+        import numpy as np
+        n = len(src)
+        a = [np.ascontiguousarray(x, dt) for x, dt in ((src, np.uint32), (dst, np.uint32), (dport, np.uint16),
+                                                       (proto, np.uint8))]
+        out = np.empty(n, np.uint32)
+        p = lambda x: x.ctypes.data_as(C.c_void_p)
+        self._ck(lib.pg_debug_walk_blob(self.h, _b(acl_name), p(a[0]), p(a[1]), p(a[2]), p(a[3]), n, p(out)))
+        return out
+
     def slot_of_rule(self, tid, idx):
         """counter slot of rule ``idx`` of table ``tid`` (idx -1: the table's default deny)."""
         base, n, dflt = self.table_info(tid)
