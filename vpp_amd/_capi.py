@@ -7,6 +7,14 @@ fails loudly, so nothing can silently run on the CPU.
 import ctypes as C
 import os
 
+try:
+    # torch wheels bundle their own HIP runtime under the same SONAME (libamdhip64.so.7) as
+    # /opt/rocm's; whichever is loaded first serves the whole process. Load torch's first so
+    # torch-allocated HBM, torch streams and these kernels share one runtime.
+    import torch  # noqa: F401
+except ImportError:  # C-ABI users without torch (e.g. a cgo host) use the system runtime
+    pass
+
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libpolicygpu.so")
 
