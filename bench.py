@@ -70,22 +70,26 @@ def main():
 
     for _ in range(a.warmup):
         D.classify(e, w.mode, w.table_id, b, out, counters=cptr)
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
+    # HIP events on the stream the kernel is launched on (torch's current stream, which
+    # D.classify passes to pg_classify), bracketing the K back-to-back launches: the
+    # per-launch average includes the inter-launch gaps, so it is an upper bound of the
+    # kernel duration rocprofv3 reports.
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for s0, s1 in evs:
-        s0.record()
+    ev0.record()
+    for _ in range(a.steps):
         D.classify(e, w.mode, w.table_id, b, out, counters=cptr)
-        s1.record()
+    ev1.record()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
-    kern_ms = float(np.mean([s0.elapsed_time(s1) for s0, s1 in evs]))
+    kern_ms = ev0.elapsed_time(ev1) / a.steps
     if world > 1:
         t = torch.tensor([wall], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -106,6 +110,7 @@ def main():
         allreduce_ms = (time.perf_counter() - t1) * 1e3
 
     achieved = n * BYTES_PER_TUPLE[w.mode] / (kern_ms * 1e-3) / 1e9
+    traffic, traffic_src = pmc_traffic(a.config, n, a.counters)
     line = {
         "metric": METRIC, "value": round(mpps, 1), "unit": "Mpps", "n_gpus": world, "steps": a.steps,
         "warmup": a.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True, "scaling": "weak",
@@ -114,8 +119,9 @@ def main():
                    "tuples_per_gpu": n, "rules": st["rules"], "tables": st["tables"], "parallelism": "dp%d" % world,
                    "counters": bool(a.counters)},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                     "bytes_per_tuple": BYTES_PER_TUPLE[w.mode], "kernel_ms": round(kern_ms, 4)},
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                     "bytes_per_tuple": BYTES_PER_TUPLE[w.mode], "kernel_ms": round(kern_ms, 4),
+                     "algorithmic_bytes_per_launch": n * BYTES_PER_TUPLE[w.mode], "traffic_source": traffic_src},
     }
     if allreduce_ms is not None:
         line["counter_allreduce_ms"] = round(allreduce_ms, 3)
@@ -125,6 +131,19 @@ def main():
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def pmc_traffic(config, n, counters):
+    """HBM bytes per classify launch from the committed rocprofv3 PMC summary of this config
+    (profiles/rNN_*_config<C>_pmc.json, FETCH_SIZE/WRITE_SIZE passes, gfx950-corrected by
+    tools/prof_summary.py), scaled to this launch's tuple count; None when there is none."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_config%d_pmc.json" % config)))
+    if not files or counters:
+        return None, None
+    with open(files[-1]) as f:
+        p = json.load(f)
+    return int(p["hbm_traffic_bytes_per_launch"] * n / p["tuples_per_launch"]), os.path.basename(files[-1])
 
 
 def cpu_baseline(w, b, out, k):

@@ -135,6 +135,11 @@ typedef struct pg_renderer pg_renderer;
 typedef struct pg_txn pg_txn;
 
 pg_ctx* pg_create(int hip_device);
+/* tuning (process-wide): "blocks_per_cu" (grid = 256 CUs x value, default 4),
+ * "stage_max_words" (largest table blob staged in LDS, default 16384 = 64 KiB),
+ * "root_bits_max" (cap of the src/key trie root stride, 4..16, default 16; affects tables
+ * compiled afterwards) */
+int pg_set_tuning(const char* key, int value);
 void pg_destroy(pg_ctx* ctx);
 const char* pg_last_error(const pg_ctx* ctx);
 const char* pg_version(void);

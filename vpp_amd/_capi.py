@@ -81,6 +81,7 @@ _SIGS = {
     "pg_version": (C.c_char_p, []),
     "pg_create": (_P, [C.c_int]),
     "pg_destroy": (None, [_P]),
+    "pg_set_tuning": (C.c_int, [C.c_char_p, C.c_int]),
     "pg_last_error": (C.c_char_p, [_P]),
     "pg_set_pod_if_name": (C.c_int, [_P, C.c_char_p, C.c_char_p, C.c_char_p]),
     "pg_set_host_interconnect_if_name": (C.c_int, [_P, C.c_char_p]),

@@ -131,6 +131,16 @@ pg_ctx* pg_create(int hip_device) {
 
 void pg_destroy(pg_ctx* ctx) { delete ctx; }
 
+int pg_set_tuning(const char* key, int value) {
+    if (!key) return PG_EINVAL;
+    if (std::string(key) == "root_bits_max") {  // applies to tables compiled afterwards
+        if (value < 4 || value > 16) return PG_EINVAL;
+        set_root_bits_max((uint32_t)value);
+        return PG_OK;
+    }
+    return dev_set_tuning(key, value) == 0 ? PG_OK : PG_EINVAL;
+}
+
 const char* pg_last_error(const pg_ctx* ctx) { return ctx ? ctx->eng.last_error.c_str() : "null context"; }
 
 int pg_set_pod_if_name(pg_ctx* ctx, const char* ns, const char* name, const char* if_name) {

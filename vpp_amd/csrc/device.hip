@@ -304,6 +304,25 @@ __device__ __forceinline__ uint32_t classify_one(const DevTableSet& T, int32_t t
 constexpr int kBlock = 256;
 constexpr uint32_t kLdsHistMax = 16384;  // slots kept in LDS (64 KiB)
 
+// Tuple streams are read once and verdicts written once: issued with the non-temporal
+// policy (A/B in one process with tools/sweep.py: +3-4 % on config 2; PG_NT_STREAM=0 builds
+// the plain-policy variant).
+typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+typedef uint32_t v2u __attribute__((ext_vector_type(2)));
+#ifndef PG_NT_STREAM
+#define PG_NT_STREAM 1
+#endif
+template <class V>
+__device__ __forceinline__ V stream_load(const V* p) {
+    if (PG_NT_STREAM) return __builtin_nontemporal_load(p);
+    return *p;
+}
+template <class V>
+__device__ __forceinline__ void stream_store(V v, V* p) {
+    if (PG_NT_STREAM) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+
 // STAGE (SINGLE mode only): the table's blob (stage_words u32, multiple of 4) is copied into
 // LDS once per workgroup and every lookup of the grid-stride loop reads it from there.
 template <int MODE, bool COUNT, bool VEC, bool STAGE>
@@ -336,30 +355,49 @@ __global__ __launch_bounds__(kBlock) void k_classify(DevTableSet T, int32_t t, c
     }
     if (STAGE || (COUNT && use_lds)) __syncthreads();
     if (MODE == 0 && !sg.linear) sg.hdr = load_hdr(sg.b);
-    const uint64_t nq = (n + 3) >> 2;
     const uint64_t stride = (uint64_t)gridDim.x * kBlock;
-    for (uint64_t q = (uint64_t)blockIdx.x * kBlock + threadIdx.x; q < nq; q += stride) {
+    const uint64_t first = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    // full quads: software-pipelined -- the next quad's 44 bytes are in flight while this
+    // quad is classified (16-B src/dst, 8-B ports, 4-B protocols per lane, coalesced)
+    const uint64_t nfull = VEC ? (n >> 2) : 0;
+    struct Quad {
+        v4u s, d;
+        v2u dp, sp;
+        uint32_t pr;
+    };
+    auto load = [&](uint64_t q) {
+        Quad x;
         const uint64_t i0 = q << 2;
-        if (VEC && i0 + 4 <= n) {
-            const uint4 s = *reinterpret_cast<const uint4*>(src + i0);
-            const uint4 d = *reinterpret_cast<const uint4*>(dst + i0);
-            const uint2 dp = *reinterpret_cast<const uint2*>(dport + i0);
-            const uint32_t pr = *reinterpret_cast<const uint32_t*>(proto + i0);
-            uint2 sp = make_uint2(0, 0);
-            if (MODE == 2) sp = *reinterpret_cast<const uint2*>(sport + i0);
-            uint4 o;
-            o.x = classify_one<MODE, COUNT>(T, t, sg, s.x, d.x, sp.x & 0xFFFFu, dp.x & 0xFFFFu, pr & 0xFFu, h);
-            o.y = classify_one<MODE, COUNT>(T, t, sg, s.y, d.y, sp.x >> 16, dp.x >> 16, (pr >> 8) & 0xFFu, h);
-            o.z = classify_one<MODE, COUNT>(T, t, sg, s.z, d.z, sp.y & 0xFFFFu, dp.y & 0xFFFFu, (pr >> 16) & 0xFFu,
-                                            h);
-            o.w = classify_one<MODE, COUNT>(T, t, sg, s.w, d.w, sp.y >> 16, dp.y >> 16, pr >> 24, h);
-            *reinterpret_cast<uint4*>(out + i0) = o;
-        } else {
-            for (uint64_t i = i0; i < n && i < i0 + 4; i++)
-                out[i] = classify_one<MODE, COUNT>(T, t, sg, src[i], dst[i], MODE == 2 ? sport[i] : 0u, dport[i],
-                                                   proto[i], h);
-        }
+        x.s = stream_load(reinterpret_cast<const v4u*>(src + i0));
+        x.d = stream_load(reinterpret_cast<const v4u*>(dst + i0));
+        x.dp = stream_load(reinterpret_cast<const v2u*>(dport + i0));
+        x.pr = stream_load(reinterpret_cast<const uint32_t*>(proto + i0));
+        x.sp = MODE == 2 ? stream_load(reinterpret_cast<const v2u*>(sport + i0)) : v2u{0u, 0u};
+        return x;
+    };
+    uint64_t q = first;
+    Quad cur;
+    if (q < nfull) cur = load(q);
+    while (q < nfull) {
+        const uint64_t qn = q + stride;
+        Quad nxt = cur;
+        if (qn < nfull) nxt = load(qn);
+        v4u o;
+        o.x = classify_one<MODE, COUNT>(T, t, sg, cur.s.x, cur.d.x, cur.sp.x & 0xFFFFu, cur.dp.x & 0xFFFFu,
+                                        cur.pr & 0xFFu, h);
+        o.y = classify_one<MODE, COUNT>(T, t, sg, cur.s.y, cur.d.y, cur.sp.x >> 16, cur.dp.x >> 16,
+                                        (cur.pr >> 8) & 0xFFu, h);
+        o.z = classify_one<MODE, COUNT>(T, t, sg, cur.s.z, cur.d.z, cur.sp.y & 0xFFFFu, cur.dp.y & 0xFFFFu,
+                                        (cur.pr >> 16) & 0xFFu, h);
+        o.w = classify_one<MODE, COUNT>(T, t, sg, cur.s.w, cur.d.w, cur.sp.y >> 16, cur.dp.y >> 16, cur.pr >> 24, h);
+        stream_store(o, reinterpret_cast<v4u*>(out + (q << 2)));
+        cur = nxt;
+        q = qn;
     }
+    // remainder (or everything when the pointers are not vector-aligned): one tuple per lane
+    for (uint64_t i = (nfull << 2) + first; i < n; i += stride)
+        out[i] = classify_one<MODE, COUNT>(T, t, sg, src[i], dst[i], MODE == 2 ? sport[i] : 0u, dport[i], proto[i],
+                                           h);
     if (COUNT && use_lds) {
         __syncthreads();
         for (uint32_t i = threadIdx.x; i < T.n_slots; i += kBlock) {
@@ -484,12 +522,20 @@ __global__ void k_conn_queries(DevTableSet T, const ConnQueryDev* q, uint32_t n,
 }
 
 // ---- launchers --------------------------------------------------------------------------------
-static int grid_for(uint64_t items) {
-    uint64_t g = (items + kBlock - 1) / kBlock;
-    return (int)std::max<uint64_t>(1, std::min<uint64_t>(g, 256ull * 8ull));
+static uint32_t g_blocks_per_cu = 4;        // grid = min(work, 256 CUs x this), grid-stride beyond
+static uint32_t g_stage_max_words = 16384;  // blobs up to 64 KiB are staged in LDS
+
+int dev_set_tuning(const std::string& key, int value) {
+    if (key == "blocks_per_cu" && value > 0 && value <= 64) g_blocks_per_cu = (uint32_t)value;
+    else if (key == "stage_max_words" && value >= 0 && value <= 36864) g_stage_max_words = (uint32_t)value;
+    else return -1;
+    return 0;
 }
 
-constexpr uint32_t kStageMaxWords = 16384;  // blobs up to 64 KiB are staged in LDS
+static int grid_for(uint64_t items) {
+    uint64_t g = (items + kBlock - 1) / kBlock;
+    return (int)std::max<uint64_t>(1, std::min<uint64_t>(g, 256ull * g_blocks_per_cu));
+}
 
 template <int MODE, bool COUNT, bool VEC>
 static void launch_classify(const DevTableSet& T, int t, const uint32_t* src, const uint32_t* dst,
@@ -499,7 +545,7 @@ static void launch_classify(const DevTableSet& T, int t, const uint32_t* src, co
     uint32_t stage = 0;
     if (MODE == 0) {
         const DevTable& hd = T.host_tabs[t];
-        if (!(hd.flags & kFlagLinear) && hd.blob_words <= kStageMaxWords) stage = hd.blob_words;
+        if (!(hd.flags & kFlagLinear) && hd.blob_words <= g_stage_max_words) stage = hd.blob_words;
     }
     const dim3 grid(grid_for((n + 3) / 4));
     if (stage)

@@ -68,6 +68,7 @@ struct HostTableSet {
 // fastpath.cpp: classification blob of one table (false = does not fit the budgets)
 bool build_fast_table(const DevRule* rules, uint32_t n, uint32_t rule_base, uint32_t default_slot,
                       std::vector<uint32_t>& blob, uint64_t cross_budget);
+void set_root_bits_max(uint32_t bits);  // cap of the tries' root stride (4..16)
 
 struct GenParams {         // device view of pg_gen_spec
     uint64_t seed, index_base;
@@ -104,6 +105,7 @@ int dev_gen(const DevTableSet& T, const GenParams& g, uint64_t n, uint32_t* src,
 int dev_conn_queries(const DevTableSet& T, const ConnQueryDev* q_host, size_t n, uint32_t* out_host,
                      std::string* err);
 int dev_set_device(int dev, std::string* err);
+int dev_set_tuning(const std::string& key, int value);
 void* dev_alloc(size_t bytes, std::string* err);
 void dev_release(void* p);
 int dev_memset(void* p, int v, size_t bytes, void* stream, std::string* err);

@@ -93,9 +93,13 @@ uint32_t build_trie(std::vector<uint32_t>& blob, const std::vector<uint64_t>& bn
     return root;
 }
 
+uint32_t g_root_bits_max = 16;
+
+// root stride: enough root entries (~4 per interval boundary) that most lookups end at the
+// root or one level below, capped (a 2^16-entry root is 256 KiB)
 uint32_t pick_stride(size_t nb, uint32_t W) {
     uint32_t s = 4;
-    while (s < 16 && s < W && (1ull << s) < 4 * (uint64_t)nb) s += 4;
+    while (s < g_root_bits_max && s < W && (1ull << s) < 4 * (uint64_t)nb) s += 4;
     return std::min(s, W);
 }
 
@@ -103,6 +107,8 @@ bool unconditional(const DevRule& r) { return r.dmask == 0 && r.klo == 0 && r.kh
 bool live(const DevRule& r) { return r.klo <= r.khi; }  // can match a TCP/UDP/OTHER packet
 
 }  // namespace
+
+void set_root_bits_max(uint32_t bits) { g_root_bits_max = std::max<uint32_t>(4, std::min<uint32_t>(16, bits)); }
 
 bool build_fast_table(const DevRule* rules, uint32_t n, uint32_t rule_base, uint32_t default_slot,
                       std::vector<uint32_t>& blob, uint64_t cross_budget) {
