@@ -352,7 +352,7 @@ class Txn:
         return None
 
     def __del__(self):
-        if getattr(self, "h", None):
+        if getattr(self, "h", None) and lib is not None:
             lib.pg_txn_free(self.h)
 
 
@@ -367,6 +367,7 @@ class Renderer:
         return Txn(self.engine, lib.pg_renderer_new_txn(self.h, int(resync)))
 
     def __del__(self):
-        if getattr(self, "h", None):
+        # at interpreter shutdown module globals may already be gone: skip, the process exits
+        if getattr(self, "h", None) and lib is not None:
             lib.pg_renderer_free(self.h)
             self.h = None
