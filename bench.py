@@ -24,6 +24,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 from vpp_amd import device as D  # noqa: E402
+from vpp_amd import dist as VD  # noqa: E402
 from vpp_amd import workloads as W  # noqa: E402
 
 METRIC = "classified 5-tuples/sec (Mpps) at 1/2/4/8 GPUs vs rule count; % of HBM peak"
@@ -47,9 +48,7 @@ def parse():
 
 def main():
     a = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    rank, world, local = VD.env()
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
@@ -60,12 +59,14 @@ def main():
     w = W.CONFIGS[a.config](local, **kw)
     e, n = w.engine, w.n_tuples
     st = w.stats()
+    base, n = VD.shard(rank, world, n)  # weak scaling: n tuples per rank, disjoint global ranges
     b = D.TupleBatch(n, with_sport=(w.mode == 2))
-    D.gen_tuples(e, b, index_base=rank * n, **w.gen)
+    D.gen_tuples(e, b, index_base=base, **w.gen)
     out = torch.empty(n, dtype=torch.int32, device="cuda")
     nslots = e.num_counter_slots()
     counters = torch.zeros(nslots, dtype=torch.int64, device="cuda")
-    cptr = counters if a.counters else None
+    use_counters = a.counters or w.counters  # config 5 runs with per-rule hit counters
+    cptr = counters if use_counters else None
     torch.cuda.synchronize()
 
     for _ in range(a.warmup):
@@ -90,10 +91,7 @@ def main():
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
     kern_ms = ev0.elapsed_time(ev1) / a.steps
-    if world > 1:
-        t = torch.tensor([wall], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        wall = float(t.item())
+    wall = VD.max_over_ranks(wall, "cuda")
     ms_per_step = wall * 1e3 / a.steps
     total_tuples = n * world * a.steps
     mpps = total_tuples / wall / 1e6
@@ -105,19 +103,19 @@ def main():
         torch.cuda.synchronize()
         dist.barrier()
         t1 = time.perf_counter()
-        dist.all_reduce(counters)
+        VD.allreduce_counters(counters)
         torch.cuda.synchronize()
         allreduce_ms = (time.perf_counter() - t1) * 1e3
 
     achieved = n * BYTES_PER_TUPLE[w.mode] / (kern_ms * 1e-3) / 1e9
-    traffic, traffic_src = pmc_traffic(a.config, n, a.counters)
+    traffic, traffic_src = pmc_traffic(a.config, n, a.counters and not w.counters)
     line = {
         "metric": METRIC, "value": round(mpps, 1), "unit": "Mpps", "n_gpus": world, "steps": a.steps,
         "warmup": a.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "u32", "data": "synthetic (device-generated, counter-based splitmix64)",
         "config": {"workload": "config%d: %s" % (a.config, w.desc), "mode": MODE_NAME[w.mode],
                    "tuples_per_gpu": n, "rules": st["rules"], "tables": st["tables"], "parallelism": "dp%d" % world,
-                   "counters": bool(a.counters)},
+                   "counters": bool(use_counters)},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "bytes_per_tuple": BYTES_PER_TUPLE[w.mode], "kernel_ms": round(kern_ms, 4),
@@ -149,36 +147,48 @@ def pmc_traffic(config, n, counters):
 def cpu_baseline(w, b, out, k):
     """The oracle's evalACL/testConnection (oracle/oracle.c) timed on this host's cores over
     the first k tuples of the same workload; also checks the GPU verdicts on that sample."""
-    from oracle import fast  # cpu_baseline leg: the checker, never the thing measured on GPU
+    from oracle import fast, world  # cpu_baseline leg: the checker, never the thing measured on GPU
 
     k = min(k, b.n)
     src, dst, sport, dport, proto = b.numpy(k)
     got = out[:k].cpu().numpy().view(np.uint32)
     e = w.engine
     threads = min(16, os.cpu_count() or 1)
-    names = e.ACLNames()
-    ora = [fast.OraACL(e.GetACLByName(x)["rules"]) for x in names]
+    extra = {}
     if w.mode == 0:
+        ora = fast.OraACL(e.GetACLByName(e.ACLNames()[w.table_id])["rules"])
         t0 = time.perf_counter()
-        act, idx = fast.eval_acl(ora[w.table_id], src, dst, dport, proto, threads=threads)
+        act, idx = fast.eval_acl(ora, src, dst, dport, proto, threads=threads)
         dt = time.perf_counter() - t0
         base = e.slot_of_rule(w.table_id, 0)
         dflt = e.slot_of_rule(w.table_id, -1)
         slot = np.where(idx >= 0, base + idx.astype(np.int64), dflt).astype(np.uint32)
-        ok = bool(((got >> 30) == act.astype(np.uint32)).all() and ((got & 0x3FFFFFFF) == slot).all())
         kind = "evalACL over the same ACL (rules pre-parsed), %d threads" % threads
+        # reference-faithful variant (CIDR strings parsed per rule visit, one thread), small sample
+        kf = min(k, 1 << 16)
+        rules = e.GetACLByName(e.ACLNames()[w.table_id])["rules"]
+        t0 = time.perf_counter()
+        fast.eval_acl_faithful(rules, src[:kf], dst[:kf], dport[:kf], proto[:kf])
+        extra["faithful_1thread_mpps"] = round(kf / (time.perf_counter() - t0) / 1e6, 4)
     else:
-        raise NotImplementedError("cpu baseline for mode %d" % w.mode)
-    # reference-faithful variant (CIDR strings parsed per rule visit, one thread), small sample
-    kf = min(k, 1 << 16)
-    rules = e.GetACLByName(names[w.table_id])["rules"] if w.mode == 0 else None
-    t0 = time.perf_counter()
-    fast.eval_acl_faithful(rules, src[:kf], dst[:kf], dport[:kf], proto[:kf])
-    dtf = time.perf_counter() - t0
-    return ({"value": round(k / dt / 1e6, 3), "unit": "Mpps", "cores": threads, "kind": "port",
-             "sample": "first %d tuples of the same workload; %s" % (k, kind),
-             "faithful_1thread_mpps": round(kf / dtf / 1e6, 4)},
-            {"tuples": k, "bit_exact_action_and_rule_index": ok})
+        wd = world.World(e, w.local_ifs, w.node_if)
+        sif, dif = wd.resolve(src), wd.resolve(dst)  # interface lookup kept outside the timed call
+        t0 = time.perf_counter()
+        if w.mode == 1:
+            act, lt, li = fast.perpod(wd.acls, wd.if_out, dif, src, dst, dport, proto, threads)
+            kind = "evalACL(outbound ACL of the dst interface), rules pre-parsed, %d threads" % threads
+        else:
+            act, lt, li = fast.test_connection(wd.acls, wd.if_in, wd.if_out, sif, dif, src, dst, sport, dport, proto,
+                                               threads)
+            kind = "testConnection (up to 4 evalACL), rules pre-parsed, %d threads" % threads
+        dt = time.perf_counter() - t0
+        slot = wd.slots(lt, li)
+        kind += ", interfaces resolved beforehand"
+    ok = bool(((got >> 30) == act.astype(np.uint32)).all() and ((got & 0x3FFFFFFF) == slot).all())
+    base = {"value": round(k / dt / 1e6, 3), "unit": "Mpps", "cores": threads, "kind": "port",
+            "sample": "first %d tuples of the same workload; %s" % (k, kind)}
+    base.update(extra)
+    return base, {"tuples": k, "bit_exact_action_and_rule_index": ok}
 
 
 if __name__ == "__main__":

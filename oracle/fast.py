@@ -30,6 +30,7 @@ def _load():
     lib.ora_acl_free.argtypes = [P]
     lib.ora_eval.argtypes = [P, P, P, P, P, C.c_size_t, P, P, C.c_int]
     lib.ora_conn.argtypes = [P, P, P, P, P, P, P, P, P, P, C.c_size_t, P, P, P, C.c_int]
+    lib.ora_perpod.argtypes = [P, P, P, P, P, P, P, C.c_size_t, P, P, P, C.c_int]
     return lib
 
 
@@ -116,3 +117,17 @@ def test_connection(acls, if_in, if_out, sif, dif, src, dst, sport, dport, proto
     lib.ora_conn(C.cast(harr, C.c_void_p), _p(if_in), _p(if_out), _p(sif), _p(dif), _p(src), _p(dst), _p(sport),
                  _p(dport), _p(proto), n, _p(conn), _p(lt), _p(li), threads)
     return conn, lt, li
+
+
+def perpod(acls, if_out, dif, src, dst, dport, proto, threads=os.cpu_count() or 1):
+    """evalACL(outbound ACL of the dst interface) per tuple. Returns (ACLAction, table
+    (-1 = no ACL, -2 = unresolved interface), matched index (-1 = none))."""
+    n = len(src)
+    harr = (C.c_void_p * max(1, len(acls)))(*[a.h for a in acls])
+    cv = lambda a, dt: np.ascontiguousarray(a, dt)
+    if_out, dif = cv(if_out, np.int32), cv(dif, np.int32)
+    src, dst, dport, proto = cv(src, np.uint32), cv(dst, np.uint32), cv(dport, np.uint16), cv(proto, np.uint8)
+    act, lt, li = np.empty(n, np.int32), np.empty(n, np.int32), np.empty(n, np.int32)
+    lib.ora_perpod(C.cast(harr, C.c_void_p), _p(if_out), _p(dif), _p(src), _p(dst), _p(dport), _p(proto), n,
+                   _p(act), _p(lt), _p(li), threads)
+    return act, lt, li

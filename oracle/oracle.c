@@ -396,3 +396,39 @@ int ora_conn(const ora_acl* const* acls, const int32_t* if_in, const int32_t* if
     for (int t = 0; t < threads; t++) pthread_join(th[t], NULL);
     return 0;
 }
+
+/* ---------------- per-pod mode: evalACL(outbound ACL of dst's interface) ---------------- */
+static void* perpod_worker(void* p) {
+    conn_job* j = (conn_job*)p;
+    for (size_t i = j->lo; i < j->hi; i++) {
+        const int32_t di = j->dif[i];
+        if (di < 0) { /* interface not resolvable: FAILURE */
+            j->conn[i] = A_FAILURE; j->last_table[i] = -2; j->last_idx[i] = -1;
+            continue;
+        }
+        const int32_t t = j->if_out[di];
+        j->last_table[i] = t;
+        j->conn[i] = eval_one(t >= 0 ? j->acls[t] : NULL, j->src[i], j->dst[i], j->proto[i], j->dport[i],
+                              &j->last_idx[i]);
+    }
+    return NULL;
+}
+
+int ora_perpod(const ora_acl* const* acls, const int32_t* if_out, const int32_t* dif, const uint32_t* src,
+               const uint32_t* dst, const uint16_t* dport, const uint8_t* proto, size_t n, int32_t* out_action,
+               int32_t* out_table, int32_t* out_idx, int threads) {
+    if (threads < 1) threads = 1;
+    if (threads > 256) threads = 256;
+    pthread_t th[256];
+    conn_job jobs[256];
+    size_t per = (n + threads - 1) / threads;
+    for (int t = 0; t < threads; t++) {
+        size_t lo = t * per, hi = (t + 1) * per < n ? (t + 1) * per : n;
+        if (lo > hi) lo = hi;
+        jobs[t] = (conn_job){acls, NULL, if_out, NULL, dif, src, dst, NULL, dport, proto, out_action, out_table,
+                             out_idx, lo, hi};
+        pthread_create(&th[t], NULL, perpod_worker, &jobs[t]);
+    }
+    for (int t = 0; t < threads; t++) pthread_join(th[t], NULL);
+    return 0;
+}

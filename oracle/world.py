@@ -1,0 +1,63 @@
+"""The installed ACLs and interface bindings of an engine, restated for the C oracle
+(TEST INFRASTRUCTURE ONLY; see oracle/__init__.py).
+
+Interface resolution follows MockACLEngine (aclengine_mock.go:273-420): an IP of a local pod
+leaves/enters through that pod's TAP; any other IP (remote pod, Internet) through the
+node-output interface (VXLAN BVI if set, else the main interface). The engine is only read
+through its public introspection calls (ACL names, ACL dumps, interface bindings, slot
+layout), never through its classifier.
+"""
+import numpy as np
+
+from . import fast
+
+
+class World:
+    def __init__(self, engine, local_ifs, node_if):
+        """local_ifs: {IPv4 u32: TAP name} of the pods on this node; node_if: name or None."""
+        self.names = engine.ACLNames()
+        self.acls = [fast.OraACL(engine.GetACLByName(n)["rules"]) for n in self.names]
+        tix = {n: i for i, n in enumerate(self.names)}
+        ifnames = sorted(set(local_ifs.values()) | ({node_if} if node_if else set()))
+        self.ifx = {x: i for i, x in enumerate(ifnames)}
+        bind = [engine._if_acls(x) for x in ifnames]
+        self.if_in = np.array([tix.get(b[0], -1) for b in bind], np.int32)
+        self.if_out = np.array([tix.get(b[1], -1) for b in bind], np.int32)
+        ips = sorted(local_ifs)
+        self.local_ips = np.array(ips, np.uint32)
+        self.local_if = np.array([self.ifx[local_ifs[ip]] for ip in ips], np.int32)
+        self.node = self.ifx[node_if] if node_if else -1
+        # slot layout of the engine (pg_table_info / pg_num_counter_slots)
+        info = [engine.table_info(engine.table_id(n)) for n in self.names]
+        self.base = np.array([b for b, _, _ in info] + [0], np.int64)
+        self.dflt = np.array([d for _, _, d in info] + [0], np.int64)
+        ns = engine.num_counter_slots()
+        self.slot_noacl, self.slot_unresolved = ns - 2, ns - 1
+
+    def resolve(self, ips):
+        ips = np.ascontiguousarray(ips, np.uint32)
+        if len(self.local_ips) == 0:
+            return np.full(len(ips), self.node, np.int32)
+        k = np.minimum(np.searchsorted(self.local_ips, ips), len(self.local_ips) - 1)
+        return np.where(self.local_ips[k] == ips, self.local_if[k], self.node).astype(np.int32)
+
+    def slots(self, table, idx):
+        """(oracle table, matched index) -> engine counter slot."""
+        table = np.asarray(table, np.int64)
+        idx = np.asarray(idx, np.int64)
+        t = np.where(table >= 0, table, len(self.names))
+        s = np.where(idx >= 0, self.base[t] + idx, self.dflt[t])
+        s = np.where(table == -1, self.slot_noacl, s)
+        s = np.where(table == -2, self.slot_unresolved, s)
+        return s.astype(np.uint32)
+
+    def perpod(self, src, dst, dport, proto, threads=1):
+        """-> (ACLAction, slot) of evalACL(outbound ACL of dst's interface)."""
+        act, lt, li = fast.perpod(self.acls, self.if_out, self.resolve(dst), src, dst, dport, proto, threads)
+        return act, self.slots(lt, li)
+
+    def conn(self, src, dst, sport, dport, proto, threads=1):
+        """-> (ConnAction, slot of the deciding evaluation) of testConnection."""
+        c, lt, li = fast.test_connection(self.acls, self.if_in, self.if_out, self.resolve(src), self.resolve(dst),
+                                         src, dst, sport, dport, proto, threads)
+        return c, self.slots(lt, li)

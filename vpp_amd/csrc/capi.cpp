@@ -342,9 +342,18 @@ int pg_sync_tables(pg_ctx* ctx) {
     GUARD_END(ctx)
 }
 
+// Table / slot metadata comes from the host image of the table set: compile, no upload
+// (usable without a GPU).
+static int ensure_compiled(pg_ctx* ctx) {
+    GUARD_BEGIN
+    if (!ctx->eng.compiled) ctx->eng.compile();
+    return PG_OK;
+    GUARD_END(ctx)
+}
+
 int pg_table_id(pg_ctx* ctx, const char* acl_name) {
     if (!ctx || !acl_name) return PG_EINVAL;
-    int rc = pg_sync_tables(ctx);
+    int rc = ensure_compiled(ctx);
     if (rc) return rc;
     auto it = ctx->eng.table_of_acl.find(acl_name);
     return it == ctx->eng.table_of_acl.end() ? PG_ENOENT : it->second;
@@ -352,19 +361,19 @@ int pg_table_id(pg_ctx* ctx, const char* acl_name) {
 
 int pg_num_tables(pg_ctx* ctx) {
     if (!ctx) return PG_EINVAL;
-    int rc = pg_sync_tables(ctx);
+    int rc = ensure_compiled(ctx);
     return rc ? rc : (int)ctx->eng.table_names.size();
 }
 
 int pg_num_counter_slots(pg_ctx* ctx) {
     if (!ctx) return PG_EINVAL;
-    int rc = pg_sync_tables(ctx);
-    return rc ? rc : (int)ctx->eng.counter_slots;
+    int rc = ensure_compiled(ctx);
+    return rc ? rc : (int)ctx->eng.slot_table.size();
 }
 
 int pg_slot_info(pg_ctx* ctx, uint32_t slot, int32_t* table_id, int32_t* rule_index) {
     if (!ctx) return PG_EINVAL;
-    int rc = pg_sync_tables(ctx);
+    int rc = ensure_compiled(ctx);
     if (rc) return rc;
     if (slot >= ctx->eng.slot_table.size()) return PG_EINVAL;
     if (table_id) *table_id = ctx->eng.slot_table[slot];
@@ -374,15 +383,13 @@ int pg_slot_info(pg_ctx* ctx, uint32_t slot, int32_t* table_id, int32_t* rule_in
 
 int pg_table_info(pg_ctx* ctx, int table_id, uint32_t* rule_base, uint32_t* n_rules, uint32_t* default_slot) {
     if (!ctx) return PG_EINVAL;
-    int rc = pg_sync_tables(ctx);
+    int rc = ensure_compiled(ctx);
     if (rc) return rc;
-    const DevTableSet& T = *ctx->eng.view();
-    if (table_id < 0 || (uint32_t)table_id >= T.n_tables) return fail(ctx, PG_EINVAL, "table id out of range");
-    uint32_t base = 0;
-    for (int t = 0; t < table_id; t++) base += (uint32_t)ctx->eng.by_name[ctx->eng.table_names[t]]->rules.size();
-    if (rule_base) *rule_base = base;
-    if (n_rules) *n_rules = (uint32_t)ctx->eng.by_name[ctx->eng.table_names[table_id]]->rules.size();
-    if (default_slot) *default_slot = T.n_rules + (uint32_t)table_id;
+    const HostTableSet& H = ctx->eng.host;
+    if (table_id < 0 || (size_t)table_id >= H.tabs.size()) return fail(ctx, PG_EINVAL, "table id out of range");
+    if (rule_base) *rule_base = H.tabs[table_id].rule_base;
+    if (n_rules) *n_rules = H.tabs[table_id].n_rules;
+    if (default_slot) *default_slot = (uint32_t)H.rules.size() + (uint32_t)table_id;
     return PG_OK;
 }
 

@@ -54,9 +54,13 @@ def subtract_subnet(n1, n2):
 
 
 class Workload:
-    def __init__(self, config, engine, mode, table_id, gen, n_tuples, desc, renderer=None):
+    """local_ifs {IPv4 u32: TAP} and node_if describe the node's interfaces (PERPOD/CONN)."""
+
+    def __init__(self, config, engine, mode, table_id, gen, n_tuples, desc, renderer=None, local_ifs=None,
+                 node_if="VXLAN-BVI", counters=False):
         self.config, self.engine, self.mode, self.table_id = config, engine, mode, table_id
         self.gen, self.n_tuples, self.desc, self.renderer = gen, n_tuples, desc, renderer
+        self.local_ifs, self.node_if, self.counters = local_ifs or {}, node_if, counters
 
     def stats(self):
         e = self.engine
@@ -105,7 +109,8 @@ def config1(device=0, n_tuples=1 << 20):
     pool = [ip_u32(x) for x in TESTDATA_IPS] * 4 + [ip_u32(x) for x in ("8.8.8.8", "10.10.50.1", "192.168.1.1")] * 6
     gen = dict(seed=SEEDS[1], ip_pool=np.array(pool, np.uint32), pool_pct=70, dst_pool_pct=70,
                port_pool=np.array(POPULAR_PORTS, np.uint16), port_pool_pct=50, tcp_pct=45, udp_pct=45)
-    return Workload(1, e, MODE_CONN, -1, gen, n_tuples, "TestCombinedRules tables, testConnection by IP", r)
+    return Workload(1, e, MODE_CONN, -1, gen, n_tuples, "TestCombinedRules tables, testConnection by IP", r,
+                    local_ifs={ip_u32("10.10.1.1"): "node1-tap1", ip_u32("10.10.2.1"): "node1-tap3"})
 
 
 # ---- config 2 ------------------------------------------------------------------------
@@ -200,4 +205,115 @@ def config4(device=0, n_tuples=64 << 20, n_rules=100000):
     return Workload(4, e, MODE_SINGLE, tid, gen, n_tuples, "100k-rule ACL, Zipf(1.1) first-match depth")
 
 
-CONFIGS = {1: config1, 2: config2, 4: config4}
+# ---- configs 3 and 5 -------------------------------------------------------------------
+INTERNET_HOSTS = ["8.8.8.8", "1.1.1.1", "192.168.10.5", "192.168.20.7", "10.96.0.10"]
+CLUSTER_PORTS = [80, 8080, 443, 53, 5353, 22, 9090]
+
+
+def cluster_pods(n_ns=10, pods_per_ns=100, apps=5, remote_pct=10):
+    """Pods ns<k>/app<a>-<j> with IP 10.1.k.(j+1); the last remote_pct % of every namespace
+    run on another node."""
+    pods = []
+    for k in range(n_ns):
+        for j in range(pods_per_ns):
+            remote = j >= pods_per_ns * (100 - remote_pct) // 100
+            pods.append({"id": "ns%d/app%d-%d" % (k, j % apps, j), "ns": k, "app": j % apps,
+                         "ip": (10 << 24) | (1 << 16) | (k << 8) | (j + 1), "remote": remote})
+    return pods
+
+
+def cluster_rules(pods, n_ns, apps):
+    """Per-pod ContivRule lists as the configurator would emit them for label-selector
+    policies (one ContivRule per selected peer /32 x port, IPBlock minus excepts via
+    subtractSubnet, deny-the-rest), keyed by (namespace, app).
+
+    egress (traffic to the pod, src = peer):
+      app (a+1) of the same namespace -> TCP 80, 8080
+      app a of namespace k+1          -> TCP 443
+      app (a+2) of namespaces k+3, k+5, k+7 -> UDP 53, 5353
+      192.168.0.0/16 except 192.168.10.0/24 -> TCP 22
+      deny the rest
+    ingress (traffic from the pod, dst = peer), app-0 pods only:
+      TCP 443 anywhere, UDP 53 to 10.96.0.10, TCP 80 to its namespace's /24, deny the rest
+    """
+    P, D = R.ActionPermit, R.ActionDeny
+    by = {}
+    for p in pods:
+        by.setdefault((p["ns"], p["app"]), []).append(p)
+    deny = R.ContivRule(D, R.IPNet(), R.IPNet(), R.ANY, 0, 0)
+    host = lambda ip: R.IPNet("%s/32" % ip_str(ip))
+    egress, ingress = {}, {}
+    block = subtract_subnet((ip_u32("192.168.0.0"), 16), (ip_u32("192.168.10.0"), 24))
+    for k in range(n_ns):
+        for a in range(apps):
+            rl = []
+            for q in by[(k, (a + 1) % apps)]:
+                rl += [R.ContivRule(P, host(q["ip"]), R.IPNet(), R.TCP, 0, port) for port in (80, 8080)]
+            for q in by[((k + 1) % n_ns, a)]:
+                rl.append(R.ContivRule(P, host(q["ip"]), R.IPNet(), R.TCP, 0, 443))
+            for kk in ((k + 3) % n_ns, (k + 5) % n_ns, (k + 7) % n_ns):
+                for q in by[(kk, (a + 2) % apps)]:
+                    rl += [R.ContivRule(P, host(q["ip"]), R.IPNet(), R.UDP, 0, port) for port in (53, 5353)]
+            for ip, pl in block:
+                rl.append(R.ContivRule(P, R.IPNet("%s/%d" % (ip_str(ip), pl)), R.IPNet(), R.TCP, 0, 22))
+            rl.append(deny)
+            egress[(k, a)] = rl
+            ingress[(k, a)] = [] if a else [
+                R.ContivRule(P, R.IPNet(), R.IPNet(), R.TCP, 0, 443),
+                R.ContivRule(P, R.IPNet(), R.IPNet("10.96.0.10/32"), R.UDP, 0, 53),
+                R.ContivRule(P, R.IPNet(), R.IPNet("10.1.%d.0/24" % k), R.TCP, 0, 80),
+                deny]
+    return ingress, egress
+
+
+def cluster_engine(device=0, n_ns=10, pods_per_ns=100, apps=5):
+    e = _new_engine(device)
+    pods = cluster_pods(n_ns, pods_per_ns, apps)
+    local = {}
+    for p in pods:
+        if not p["remote"]:
+            ifn = "tap-%s" % p["id"].replace("/", "-")
+            e.SetPodIfName(p["id"], ifn)
+            local[p["ip"]] = ifn
+        e.RegisterPod(p["id"], ip_str(p["ip"]), p["remote"])
+    ingress, egress = cluster_rules(pods, n_ns, apps)
+    r = R.Renderer(e)
+    t = r.NewTxn(True)
+    for p in pods:
+        if not p["remote"]:  # the renderer is told about the pods of this node
+            key = (p["ns"], p["app"])
+            t.Render(p["id"], R.IPNet.host(ip_str(p["ip"])), ingress[key], egress[key], False)
+    err = t.Commit()
+    assert err is None, err
+    pool = [p["ip"] for p in pods] + [ip_u32(x) for x in INTERNET_HOSTS] * 10
+    return e, r, local, np.array(pool, np.uint32)
+
+
+def config3(device=0, n_tuples=125 << 20):
+    e, r, local, pool = cluster_engine(device)
+    gen = dict(seed=SEEDS[3], ip_pool=pool, pool_pct=85, dst_pool_pct=88,
+               port_pool=np.array(CLUSTER_PORTS, np.uint16), port_pool_pct=80, tcp_pct=60, udp_pct=30)
+    return Workload(3, e, MODE_PERPOD, -1, gen, n_tuples,
+                    "1k pods / 10 namespaces, per-pod tables + global, evalACL on the dst interface", r,
+                    local_ifs=local)
+
+
+def config5(device=0, n_tuples=125 << 20):
+    e, r, local, pool = cluster_engine(device)
+    gen = dict(seed=SEEDS[5], ip_pool=pool, pool_pct=85, dst_pool_pct=88,
+               port_pool=np.array(CLUSTER_PORTS, np.uint16), port_pool_pct=80, tcp_pct=60, udp_pct=30)
+    return Workload(5, e, MODE_CONN, -1, gen, n_tuples,
+                    "config-3 topology, testConnection both directions, per-rule hit counters", r,
+                    local_ifs=local, counters=True)
+
+
+def table_histogram(e):
+    """rules per table -> number of tables (config 3's table-size histogram)."""
+    h = {}
+    for t in range(e.num_tables()):
+        n = e.table_info(t)[1]
+        h[n] = h.get(n, 0) + 1
+    return dict(sorted(h.items()))
+
+
+CONFIGS = {1: config1, 2: config2, 3: config3, 4: config4, 5: config5}
