@@ -135,7 +135,8 @@ typedef struct pg_renderer pg_renderer;
 typedef struct pg_txn pg_txn;
 
 pg_ctx* pg_create(int hip_device);
-/* tuning (process-wide): "blocks_per_cu" (grid = 256 CUs x value, default 4),
+/* tuning (process-wide): "blocks_per_cu" (cap on resident workgroups per CU of the classify
+ * grid; default 0 = as many as registers/LDS allow),
  * "stage_max_words" (largest table blob staged in LDS, default 16384 = 64 KiB),
  * "root_bits_max" (cap of the src/key trie root stride, 4..16, default 16; affects tables
  * compiled afterwards) */

@@ -26,7 +26,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", type=int, default=2)
     ap.add_argument("--tuples", type=int, default=0)
-    ap.add_argument("--bpc", default="2,4,8,16")
+    ap.add_argument("--bpc", default="0,2,4,8", help="0 = occupancy-sized grid")
     ap.add_argument("--stage", default="1")
     ap.add_argument("--alt", default="")
     ap.add_argument("--root", default="", help="extra contexts with these trie root caps, e.g. 8,12")

@@ -1,19 +1,28 @@
 // The walk of a classification blob (layout: fastpath.cpp), written once for both sides:
-// the HIP kernels instantiate it with a loader that issues 16/8-byte LDS or global loads,
+// the HIP kernels instantiate it with a loader that issues 16/8/4-byte LDS or global loads,
 // and pg_debug_walk_blob (tests only, never on the classify path) instantiates it with a
-// host loader so the builder can be checked against the oracle without a GPU.
+// host loader, so the table compiler is checked against the oracle without a GPU.
+//
+// The walk is "lockstep" over Q tuples (Q = 4 per lane in the kernels): every dependent
+// step (trie level, cross entry, record) issues the loads of all Q tuples before consuming
+// any of them, so a lane keeps up to 2Q independent loads in flight instead of one chain.
 #pragma once
 #include <cstdint>
 
 #if defined(__HIPCC__)
 #define PG_HD __host__ __device__ __forceinline__
+#define PG_UNROLL _Pragma("unroll")
 #else
 #define PG_HD inline
+#define PG_UNROLL _Pragma("GCC unroll 4")
 #endif
 
 namespace pg {
 
 constexpr uint32_t kFlagCross = 1u, kFlagLists = 2u, kFlagCand = 4u, kFlagLinear = 8u;
+constexpr uint32_t kLeaf = 0x80000000u;
+constexpr uint32_t kSrcRoot = 16u;       // the src trie root follows the 16-word blob header
+constexpr uint32_t kWalkKeyLimit = 0x30000u;  // keys >= this (ANY protocol) take the linear path
 
 struct W2 {
     uint32_t x, y;
@@ -22,52 +31,104 @@ struct W4 {
     uint32_t x, y, z, w;
 };
 
-struct BlobHdr {
-    uint32_t flags, dflt, sroot, s1, kroot, k1, xoff, nkc, loff, voff;
+// What a walk needs of a table (the device keeps it in DevTable, 32 B).
+struct BlobTab {
+    uint32_t fsk;    // flags | s1 << 8 | k1 << 16
+    uint32_t dflt;   // default verdict (DENY << 30 | default slot)
+    uint32_t kroot;  // key trie root (words)
+    uint32_t xoff;   // cross table (CROSS) or first record (CAND), words
+    uint32_t nkc;    // key classes
 };
 
-template <class L>
-PG_HD BlobHdr blob_hdr(const L& ld) {
-    const W4 a = ld.u4(0), c = ld.u4(4);
-    const W2 d = ld.u2(8);
-    return BlobHdr{a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w, d.x, d.y};
+// Record (16 B): {dnet, klo | dlen << 18, khi, verdict}: matches when the dst prefix of
+// length dlen equals dnet and klo <= key <= khi. Candidate lists (CAND) and dst lists (LISTS)
+// end with a record that matches every packet and carries the fall-through verdict.
+PG_HD uint32_t rec_mask(uint32_t dlen) { return dlen ? (0xFFFFFFFFu << (32u - dlen)) : 0u; }
+PG_HD bool rec_match(const W4& r, uint32_t dst, uint32_t key) {
+    return (dst & rec_mask((r.y >> 18) & 63u)) == r.x && key >= (r.y & 0x3FFFFu) && key <= r.z;
 }
 
-// multibit trie: root stride s1 over a W-bit value, then 8-bit strides; bit 31 marks a leaf
-template <class L>
-PG_HD uint32_t blob_trie(const L& ld, uint32_t root, uint32_t s1, uint32_t W, uint32_t x) {
-    uint32_t shift = W - s1;
-    uint32_t e = ld.u32(root + (x >> shift));
-    while (!(e & 0x80000000u)) {
-        const uint32_t st = shift < 8u ? shift : 8u;
-        shift -= st;
-        e = ld.u32(e + ((x >> shift) & ((1u << st) - 1u)));
-    }
-    return e & 0x7FFFFFFFu;
-}
-
-// evalACL over a table's blob for TCP/UDP/OTHER packets (key < 0x30000)
-template <class L>
-PG_HD uint32_t blob_eval(const L& ld, const BlobHdr& h, uint32_t src, uint32_t dst, uint32_t key) {
-    const uint32_t sc = blob_trie(ld, h.sroot, h.s1, 32u, src);
-    if (h.flags & kFlagCross) {
-        const uint32_t kc = blob_trie(ld, h.kroot, h.k1, 18u, key);
-        const uint32_t idx = sc * h.nkc + kc;
-        if (!(h.flags & kFlagLists)) return ld.u32(h.xoff + idx);
-        const W2 e = ld.u2(h.xoff + 2u * idx);
-        const uint32_t cnt = e.y & 255u;
-        for (uint32_t j = 0; j < cnt; j++) {
-            const W4 l = ld.u4((e.y >> 8) + 4u * j);
-            if ((dst & l.y) == l.x) return l.z;
+// on[j]: tuple j is walked (table present, not LINEAR, key < kWalkKeyLimit). w[j] is only
+// written for those.
+template <class L, int Q>
+PG_HD void blob_walk(const L (&ld)[Q], const BlobTab (&tb)[Q], const bool (&on)[Q], const uint32_t (&src)[Q],
+                     const uint32_t (&dst)[Q], const uint32_t (&key)[Q], uint32_t (&w)[Q]) {
+    uint32_t es[Q], ek[Q], ss[Q], sk[Q];
+    PG_UNROLL
+    for (int j = 0; j < Q; j++) {
+        es[j] = ek[j] = kLeaf;
+        ss[j] = sk[j] = 0;
+        if (on[j]) {
+            ss[j] = 32u - ((tb[j].fsk >> 8) & 0xFFu);
+            es[j] = ld[j].u32(kSrcRoot + (src[j] >> ss[j]));
+            if (tb[j].fsk & kFlagCross) {
+                sk[j] = 18u - (tb[j].fsk >> 16);
+                ek[j] = ld[j].u32(tb[j].kroot + (key[j] >> sk[j]));
+            }
         }
-        return e.x;
     }
-    const W2 c = ld.u2(h.xoff + 2u * sc);
-    for (uint32_t j = 0; j < c.y; j++) {
-        const W4 k = ld.u4(h.loff + 4u * (c.x + j));
-        if ((dst & k.y) == k.x && key >= k.z && key <= k.w) return ld.u32(h.voff + c.x + j);
+    // descend both multibit tries (root stride, then 8-bit strides) of all Q tuples together
+    for (;;) {
+        bool more = false;
+        PG_UNROLL
+        for (int j = 0; j < Q; j++) more |= !(es[j] & ek[j] & kLeaf);
+        if (!more) break;
+        PG_UNROLL
+        for (int j = 0; j < Q; j++) {
+            if (!(es[j] & kLeaf)) {
+                const uint32_t st = ss[j] < 8u ? ss[j] : 8u;
+                ss[j] -= st;
+                es[j] = ld[j].u32(es[j] + ((src[j] >> ss[j]) & ((1u << st) - 1u)));
+            }
+            if (!(ek[j] & kLeaf)) {
+                const uint32_t st = sk[j] < 8u ? sk[j] : 8u;
+                sk[j] -= st;
+                ek[j] = ld[j].u32(ek[j] + ((key[j] >> sk[j]) & ((1u << st) - 1u)));
+            }
+        }
     }
-    return h.dflt;
+    // cross entry, or the first record of the src class's candidate list
+    uint32_t pos[Q];
+    bool pend[Q];
+    PG_UNROLL
+    for (int j = 0; j < Q; j++) {
+        pend[j] = false;
+        pos[j] = 0;
+        if (!on[j]) continue;
+        const uint32_t sc = es[j] & ~kLeaf;
+        if (tb[j].fsk & kFlagCross) {
+            const uint32_t idx = sc * tb[j].nkc + (ek[j] & ~kLeaf);
+            if (!(tb[j].fsk & kFlagLists)) {
+                w[j] = ld[j].u32(tb[j].xoff + idx);
+            } else {
+                const W2 e = ld[j].u2(tb[j].xoff + 2u * idx);
+                w[j] = e.x;
+                pos[j] = e.y;  // 0: no dst-specific rule ahead of the verdict
+                pend[j] = e.y != 0u;
+            }
+        } else {
+            pos[j] = tb[j].xoff + 4u * sc;
+            pend[j] = true;
+        }
+    }
+    // records until the first match (every list ends with a match-all record)
+    for (;;) {
+        bool more = false;
+        PG_UNROLL
+        for (int j = 0; j < Q; j++) more |= pend[j];
+        if (!more) break;
+        PG_UNROLL
+        for (int j = 0; j < Q; j++) {
+            if (!pend[j]) continue;
+            const W4 r = ld[j].u4(pos[j]);
+            if (rec_match(r, dst[j], key[j])) {
+                w[j] = r.w;
+                pend[j] = false;
+            } else {
+                pos[j] += 4u;
+            }
+        }
+    }
 }
 
 struct HostLoader {

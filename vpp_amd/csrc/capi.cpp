@@ -401,11 +401,12 @@ int pg_table_stats(pg_ctx* ctx, int table_id, uint32_t* flags, uint32_t* blob_by
     if (!E.compiled) E.compile();
     if (table_id < 0 || (size_t)table_id >= E.host.tabs.size()) return fail(ctx, PG_EINVAL, "table id out of range");
     const DevTable& hd = E.host.tabs[table_id];
+    const uint32_t words = E.host.blob_words[table_id];
     const uint32_t* b = E.host.blobs.data() + hd.blob_off;
-    if (flags) *flags = hd.flags;
-    if (blob_bytes) *blob_bytes = hd.blob_words * 4;
-    if (n_src_classes) *n_src_classes = hd.blob_words ? b[10] : 0;
-    if (n_key_classes) *n_key_classes = (hd.blob_words && (hd.flags & kFlagCross)) ? b[7] : 0;
+    if (flags) *flags = hd.fsk & 0xFFu;
+    if (blob_bytes) *blob_bytes = words * 4;
+    if (n_src_classes) *n_src_classes = words ? b[10] : 0;
+    if (n_key_classes) *n_key_classes = (words && (hd.fsk & kFlagCross)) ? b[7] : 0;
     return PG_OK;
     GUARD_END(ctx)
 }
@@ -419,32 +420,49 @@ int pg_debug_walk_blob(pg_ctx* ctx, const char* acl_name, const uint32_t* src, c
     auto it = E.table_of_acl.find(acl_name);
     if (it == E.table_of_acl.end()) return fail(ctx, PG_ENOENT, "no such ACL");
     const DevTable& hd = E.host.tabs[it->second];
-    const uint32_t NR = (uint32_t)E.host.rules.size();
-    HostLoader ld{E.host.blobs.data() + hd.blob_off};
-    BlobHdr bh{};
-    if (!(hd.flags & kFlagLinear)) bh = blob_hdr(ld);
-    for (uint64_t i = 0; i < n; i++) {
-        uint32_t key = pkt_key_host(proto[i], dst_port[i]);
-        if (proto[i] > 2) key = kKeyANY;
-        if (!(hd.flags & kFlagLinear) && key < kKeyANY) {
-            out[i] = blob_eval(ld, bh, src[i], dst[i], key);
-            continue;
+    const bool linear = (hd.fsk & kFlagLinear) != 0;
+    // the kernels' lockstep walk, 4 tuples at a time
+    constexpr int Q = 4;
+    HostLoader ld[Q];
+    BlobTab tb[Q];
+    for (int j = 0; j < Q; j++) {
+        ld[j] = HostLoader{E.host.blobs.data() + hd.blob_off};
+        tb[j] = BlobTab{hd.fsk, hd.dflt, hd.kroot, hd.xoff, hd.nkc};
+    }
+    for (uint64_t i0 = 0; i0 < n; i0 += Q) {
+        bool on[Q];
+        uint32_t s4[Q], d4[Q], k4[Q], w4[Q];
+        for (int j = 0; j < Q; j++) {
+            const uint64_t i = i0 + j;
+            const bool in = i < n;
+            s4[j] = in ? src[i] : 0;
+            d4[j] = in ? dst[i] : 0;
+            k4[j] = in ? (proto[i] > 2 ? kKeyANY : pkt_key_host(proto[i], dst_port[i])) : 0;
+            on[j] = in && !linear && k4[j] < kWalkKeyLimit;
+            w4[j] = 0;
         }
-        uint32_t w = (kActDeny << 30) | (NR + (uint32_t)it->second);  // mirror of eval_linear_lane
-        for (uint32_t r = 0; r < hd.n_rules; r++) {
-            const DevRule& R = E.host.rules[hd.rule_base + r];
-            if ((src[i] & R.smask) != R.snet || (dst[i] & R.dmask) != R.dnet) continue;
-            if (key >= kKeyANY) {
-                if ((R.act >> 4) == kActNever) continue;
-                w = (((R.act >> 4) & 3u) << 30) | (hd.rule_base + r);
-                break;
+        blob_walk(ld, tb, on, s4, d4, k4, w4);
+        for (int j = 0; j < Q && i0 + j < n; j++) {
+            if (on[j]) {
+                out[i0 + j] = w4[j];
+                continue;
             }
-            if (key >= R.klo && key <= R.khi) {
-                w = ((R.act & 3u) << 30) | (hd.rule_base + r);
-                break;
+            uint32_t w = hd.dflt;  // mirror of eval_linear_lane
+            for (uint32_t r = 0; r < hd.n_rules; r++) {
+                const DevRule& R = E.host.rules[hd.rule_base + r];
+                if ((s4[j] & R.smask) != R.snet || (d4[j] & R.dmask) != R.dnet) continue;
+                if (k4[j] >= kKeyANY) {
+                    if ((R.act >> 4) == kActNever) continue;
+                    w = (((R.act >> 4) & 3u) << 30) | (hd.rule_base + r);
+                    break;
+                }
+                if (k4[j] >= R.klo && k4[j] <= R.khi) {
+                    w = ((R.act & 3u) << 30) | (hd.rule_base + r);
+                    break;
+                }
             }
+            out[i0 + j] = w;
         }
-        out[i] = w;
     }
     return PG_OK;
     GUARD_END(ctx)

@@ -2,13 +2,16 @@
 //
 //  K1 k_linear       reference-shaped first-match scan: one lane per tuple, rules read
 //                    wave-uniformly (scalar loads), wave exits when every lane matched.
-//  K2 k_classify     the production path for SINGLE / PERPOD / CONN modes: src-interval
-//                    lookup (radix + short binary search) then a scan of that interval's
-//                    candidate list (dst + L4 tests only); 4 tuples per lane with 16/8/4-byte
-//                    coalesced SoA loads; per-rule hit counters kept in an LDS histogram
-//                    and flushed once per workgroup with u64 atomics (K6).
-//  K3 (inside K2)    CONN mode fuses testConnection's up-to-4 evalACL lookups
-//                    (mock/aclengine/aclengine_mock.go:424-501).
+//  K2 k_classify     the production path for SINGLE / PERPOD / CONN modes: per table a
+//                    classification blob (fastpath.cpp: src/key multibit tries -> equivalence
+//                    classes -> cross-product verdicts or candidate records), walked for 4
+//                    tuples per lane in lockstep (blobwalk.hpp) after 16/8/4-byte coalesced,
+//                    non-temporal SoA loads of the quad; SINGLE mode stages the blob in LDS;
+//                    per-rule hit counters kept in an LDS histogram and flushed once per
+//                    workgroup with u64 atomics.
+//  K3 (inside K2)    PERPOD / CONN: IPv4 -> interface + its ACL tables by one 16-B hash probe;
+//                    CONN fuses testConnection's up-to-4 evalACL steps
+//                    (mock/aclengine/aclengine_mock.go:424-501), each in lockstep over the quad.
 //  K5 k_gen          counter-based (splitmix64) synthetic 5-tuple generator.
 //
 // Semantics of one evaluation == evalACL (aclengine_mock.go:503-652) over the ACL the table
@@ -37,6 +40,7 @@ struct DeviceBuffers {
     void* blob = nullptr;
     DevTableSet view{};
     std::vector<DevTable> host_tabs;
+    std::vector<uint32_t> host_blob_words;
 };
 
 const DevTableSet& dev_view(const DeviceBuffers* b) { return b->view; }
@@ -117,6 +121,8 @@ DeviceBuffers* dev_upload(const HostTableSet& h, std::string* err) {
     v.iphash = (const uint32_t*)(base + o_ip);
     v.iphash_mask = h.iphash_mask;
     v.node_if = h.node_if;
+    v.node_in = h.node_in;
+    v.node_out = h.node_out;
     v.n_rules = (uint32_t)h.rules.size();
     v.n_tables = (uint32_t)h.tabs.size();
     v.n_ifaces = (uint32_t)(h.ifaces.size() / 2);
@@ -124,7 +130,9 @@ DeviceBuffers* dev_upload(const HostTableSet& h, std::string* err) {
     v.slot_unresolved = v.slot_noacl + 1;
     v.n_slots = v.slot_unresolved + 1;
     b->host_tabs = h.tabs;
+    b->host_blob_words = h.blob_words;
     v.host_tabs = b->host_tabs.data();
+    v.host_blob_words = b->host_blob_words.data();
     return b;
 }
 
@@ -142,27 +150,26 @@ __device__ __forceinline__ uint32_t pkt_key(uint32_t proto, uint32_t port) {
     return proto == 0u ? port : (proto == 1u ? (kKeyUDP | port) : (proto == 2u ? kKeyOTHER : kKeyANY));
 }
 __device__ __forceinline__ uint32_t verdict(uint32_t act, uint32_t slot) { return (act << 30) | slot; }
+constexpr uint32_t kSlotMask = 0x3FFFFFFFu;
 
-// Linear first-match over a table's compiled rules (fallback for tables whose candidate
-// lists would exceed the budget; also the ANY-packet path).
-__device__ __noinline__ uint32_t eval_linear_lane(const DevTableSet& T, uint32_t t, uint32_t src, uint32_t dst,
-                                                  uint32_t key) {
-    const DevTable hd = T.tabs[t];
+// Linear first-match over a table's compiled rules: LINEAR tables and ANY-protocol packets
+// (rare). Scalar arguments only, so the call needs no stack frame.
+__device__ __noinline__ uint32_t eval_linear(const DevRule* rules, uint32_t base, uint32_t nr, uint32_t dflt,
+                                             uint32_t src, uint32_t dst, uint32_t key) {
     const bool any = key >= kKeyANY;
-    for (uint32_t i = 0; i < hd.n_rules; i++) {
-        const DevRule r = T.rules[hd.rule_base + i];
+    for (uint32_t i = 0; i < nr; i++) {
+        const DevRule r = rules[base + i];
         if ((src & r.smask) != r.snet || (dst & r.dmask) != r.dnet) continue;
         if (any) {
-            if ((r.act >> 4) != kActNever) return verdict((r.act >> 4) & 3u, hd.rule_base + i);
+            if ((r.act >> 4) != kActNever) return verdict((r.act >> 4) & 3u, base + i);
         } else if (key >= r.klo && key <= r.khi) {
-            return verdict(r.act & 3u, hd.rule_base + i);
+            return verdict(r.act & 3u, base + i);
         }
     }
-    return verdict(kActDeny, T.n_rules + t);
+    return dflt;
 }
 
-// ---- classification blob walk (layout: fastpath.cpp, walk: blobwalk.hpp) -----------------------
-struct DevLoader {  // 16/8-byte loads; LDS or global depending on where the pointer came from
+struct DevLoader {  // 16/8/4-byte loads from LDS or global memory (address space inferred)
     const uint32_t* b;
     __device__ __forceinline__ uint32_t u32(uint32_t i) const { return b[i]; }
     __device__ __forceinline__ W2 u2(uint32_t i) const {
@@ -174,21 +181,40 @@ struct DevLoader {  // 16/8-byte loads; LDS or global depending on where the poi
         return W4{v.x, v.y, v.z, v.w};
     }
 };
-__device__ __forceinline__ BlobHdr load_hdr(const uint32_t* b) { return blob_hdr(DevLoader{b}); }
-__device__ __forceinline__ uint32_t eval_blob(const uint32_t* b, const BlobHdr& h, uint32_t src, uint32_t dst,
-                                              uint32_t key) {
-    return blob_eval(DevLoader{b}, h, src, dst, key);
+
+__device__ __forceinline__ DevTable load_tab(const DevTable* tabs, int32_t t) {
+    const uint4* p = reinterpret_cast<const uint4*>(tabs + t);
+    const uint4 a = p[0], c = p[1];
+    return DevTable{a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w};
 }
 
-// evalACL(table t) -- t < 0: no ACL on the interface (PERMIT, aclengine_mock.go:506-508)
-__device__ __forceinline__ uint32_t eval_table(const DevTableSet& T, int32_t t, uint32_t src, uint32_t dst,
-                                               uint32_t key) {
-    if (t < 0) return verdict(kActPermit, T.slot_noacl);
-    const DevTable hd = T.tabs[t];
-    if ((hd.flags & kFlagLinear) || key >= kKeyANY) return eval_linear_lane(T, (uint32_t)t, src, dst, key);
-    const uint32_t* b = T.blobs + hd.blob_off;
-    return eval_blob(b, load_hdr(b), src, dst, key);
+// evalACL (aclengine_mock.go:503-652) of Q tuples against their tables, in lockstep.
+// act[j]: evaluate tuple j against tab[j]; blobs: base the tables' blob_off is relative to
+// (the global blob array, or the LDS copy of a staged table).
+template <int Q>
+__device__ __forceinline__ void eval_q(const DevTableSet& T, const uint32_t* blobs, const DevTable (&tab)[Q],
+                                       const bool (&act)[Q], const uint32_t (&src)[Q], const uint32_t (&dst)[Q],
+                                       const uint32_t (&key)[Q], uint32_t (&w)[Q]) {
+    DevLoader ld[Q];
+    BlobTab tb[Q];
+    bool on[Q];
+#pragma unroll
+    for (int j = 0; j < Q; j++) {
+        ld[j] = DevLoader{blobs + tab[j].blob_off};
+        tb[j] = BlobTab{tab[j].fsk, tab[j].dflt, tab[j].kroot, tab[j].xoff, tab[j].nkc};
+        on[j] = act[j] && !(tab[j].fsk & kFlagLinear) && key[j] < kWalkKeyLimit;
+    }
+    blob_walk(ld, tb, on, src, dst, key, w);
+#pragma unroll
+    for (int j = 0; j < Q; j++)
+        if (act[j] && !on[j])
+            w[j] = eval_linear(T.rules, tab[j].rule_base, tab[j].n_rules, tab[j].dflt, src[j], dst[j], key[j]);
 }
+
+// tables of a connection end point: interface (-1/-2 unresolvable) and its ACLs
+struct End {
+    int32_t ifc, tin, tout;
+};
 
 __device__ __forceinline__ uint32_t hash_ip(uint32_t ip) {
     ip ^= ip >> 16;
@@ -198,14 +224,38 @@ __device__ __forceinline__ uint32_t hash_ip(uint32_t ip) {
     ip ^= ip >> 16;
     return ip;
 }
-// IPv4 -> interface: local pod TAP, else the node-output interface (VXLAN BVI or main)
-__device__ __forceinline__ int32_t iface_by_ip(const DevTableSet& T, uint32_t ip) {
-    uint32_t s = hash_ip(ip) & T.iphash_mask;
+// IPv4 -> end point: a local pod's TAP, else the node-output interface (VXLAN BVI or main;
+// aclengine_mock.go:273-420). Q probes in lockstep, one 16-B load per probe step.
+template <int Q>
+__device__ __forceinline__ void probe_q(const DevTableSet& T, const uint32_t (&ip)[Q], End (&e)[Q]) {
+    const uint4* H = reinterpret_cast<const uint4*>(T.iphash);
+    uint32_t s[Q];
+    uint4 v[Q];
+    bool pend[Q];
+#pragma unroll
+    for (int j = 0; j < Q; j++) {
+        s[j] = hash_ip(ip[j]) & T.iphash_mask;
+        v[j] = H[s[j]];
+        pend[j] = true;
+    }
     for (;;) {
-        const uint2 e = reinterpret_cast<const uint2*>(T.iphash)[s];
-        if (e.y == 0xFFFFFFFFu) return T.node_if;
-        if (e.x == ip) return (int32_t)e.y;
-        s = (s + 1u) & T.iphash_mask;
+        bool more = false;
+#pragma unroll
+        for (int j = 0; j < Q; j++) {
+            if (!pend[j]) continue;
+            if (v[j].y == 0xFFFFFFFFu) {
+                e[j] = End{T.node_if, T.node_in, T.node_out};
+                pend[j] = false;
+            } else if (v[j].x == ip[j]) {
+                e[j] = End{(int32_t)v[j].y, (int32_t)v[j].z, (int32_t)v[j].w};
+                pend[j] = false;
+            } else {
+                s[j] = (s[j] + 1u) & T.iphash_mask;
+                v[j] = H[s[j]];
+                more = true;
+            }
+        }
+        if (!more) break;
     }
 }
 
@@ -218,86 +268,150 @@ struct Hist {
     }
 };
 
-// testConnection (aclengine_mock.go:424-501) on resolved interfaces
-template <bool COUNT>
-__device__ __forceinline__ uint32_t test_connection(const DevTableSet& T, int32_t sif, int32_t dif, uint32_t src,
-                                                    uint32_t dst, uint32_t key_syn, uint32_t key_synack,
-                                                    const Hist& h) {
-    if (sif < 0 || dif < 0) {
-        if (COUNT) h.inc(T.slot_unresolved);
-        return verdict(3u, T.slot_unresolved);
+// one evalACL step of testConnection / per-pod mode: tables t[j] (-1 = no ACL: PERMIT)
+template <int Q, bool COUNT>
+__device__ __forceinline__ void eval_step(const DevTableSet& T, const int32_t (&t)[Q], const bool (&run)[Q],
+                                          const uint32_t (&a)[Q], const uint32_t (&b)[Q], const uint32_t (&key)[Q],
+                                          const Hist& h, uint32_t (&w)[Q]) {
+    DevTable tab[Q];
+    bool act[Q];
+#pragma unroll
+    for (int j = 0; j < Q; j++) {
+        act[j] = run[j] && t[j] >= 0;
+        tab[j] = act[j] ? load_tab(T.tabs, t[j]) : DevTable{};
+        if (run[j] && t[j] < 0) w[j] = verdict(kActPermit, T.slot_noacl);  // nil ACL (:506-508)
     }
-    const int2 si = reinterpret_cast<const int2*>(T.ifaces)[sif];
-    const int2 di = reinterpret_cast<const int2*>(T.ifaces)[dif];
-    const bool same = sif == dif;
-    bool src_refl = false, dst_refl = false;
-    uint32_t w = eval_table(T, si.x, src, dst, key_syn);  // SYN: src inbound
-    if (COUNT) h.inc(w & 0x3FFFFFFFu);
-    uint32_t a = w >> 30;
-    if (a == kActFailure) return verdict(3u, w & 0x3FFFFFFFu);
-    if (a == kActDeny) return verdict(0u, w & 0x3FFFFFFFu);
-    if (a == kActReflect) {
-        src_refl = true;
-        if (same) dst_refl = true;
+    eval_q(T, T.blobs, tab, act, a, b, key, w);
+    if (COUNT) {
+#pragma unroll
+        for (int j = 0; j < Q; j++)
+            if (run[j]) h.inc(w[j] & kSlotMask);
     }
-    if (!dst_refl) {  // SYN: dst outbound
-        w = eval_table(T, di.y, src, dst, key_syn);
-        if (COUNT) h.inc(w & 0x3FFFFFFFu);
-        a = w >> 30;
-        if (a == kActFailure) return verdict(3u, w & 0x3FFFFFFFu);
-        if (a == kActDeny) return verdict(0u, w & 0x3FFFFFFFu);
-        if (a == kActReflect) {
-            dst_refl = true;
-            if (same) src_refl = true;
-        }
-    }
-    if (!dst_refl) {  // SYN-ACK: dst inbound
-        w = eval_table(T, di.x, dst, src, key_synack);
-        if (COUNT) h.inc(w & 0x3FFFFFFFu);
-        a = w >> 30;
-        if (a == kActFailure) return verdict(3u, w & 0x3FFFFFFFu);
-        if (a == kActDeny) return verdict(1u, w & 0x3FFFFFFFu);
-    }
-    if (!src_refl) {  // SYN-ACK: src outbound
-        w = eval_table(T, si.y, dst, src, key_synack);
-        if (COUNT) h.inc(w & 0x3FFFFFFFu);
-        a = w >> 30;
-        if (a == kActFailure) return verdict(3u, w & 0x3FFFFFFFu);
-        if (a == kActDeny) return verdict(1u, w & 0x3FFFFFFFu);
-    }
-    return verdict(2u, w & 0x3FFFFFFFu);
 }
 
-// SINGLE mode: the table's blob (staged in LDS or read from HBM/L2) and its header
-struct Single {
-    const uint32_t* b;
-    BlobHdr hdr;
-    bool linear;
-};
-
-template <int MODE, bool COUNT>
-__device__ __forceinline__ uint32_t classify_one(const DevTableSet& T, int32_t t, const Single& sg, uint32_t src,
-                                                 uint32_t dst, uint32_t sport, uint32_t dport, uint32_t proto,
-                                                 const Hist& h) {
-    if (MODE == 0) {  // SINGLE
-        const uint32_t key = pkt_key(proto, dport);
-        const uint32_t w = (sg.linear || key >= kKeyANY) ? eval_linear_lane(T, (uint32_t)t, src, dst, key)
-                                                         : eval_blob(sg.b, sg.hdr, src, dst, key);
-        if (COUNT) h.inc(w & 0x3FFFFFFFu);
-        return w;
-    } else if (MODE == 1) {  // PERPOD: outbound ACL of the egress interface of dst
-        const int32_t dif = iface_by_ip(T, dst);
-        if (dif < 0) {
+// testConnection (aclengine_mock.go:424-501) of Q connections on resolved end points, each
+// of its up-to-4 evalACL steps in lockstep over the Q connections.
+template <int Q, bool COUNT>
+__device__ __forceinline__ void conn_q(const DevTableSet& T, const End (&es)[Q], const End (&ed)[Q],
+                                       const uint32_t (&src)[Q], const uint32_t (&dst)[Q], const uint32_t (&ksyn)[Q],
+                                       const uint32_t (&kack)[Q], const Hist& h, uint32_t (&out)[Q]) {
+    bool live[Q], srefl[Q], drefl[Q], same[Q], run[Q];
+    uint32_t w[Q];
+    int32_t t[Q];
+#pragma unroll
+    for (int j = 0; j < Q; j++) {
+        live[j] = es[j].ifc >= 0 && ed[j].ifc >= 0;
+        srefl[j] = drefl[j] = false;
+        same[j] = es[j].ifc == ed[j].ifc;
+        w[j] = 0;
+        if (!live[j]) {
+            out[j] = verdict(3u, T.slot_unresolved);
             if (COUNT) h.inc(T.slot_unresolved);
-            return verdict(kActFailure, T.slot_unresolved);
         }
-        const int32_t tt = reinterpret_cast<const int2*>(T.ifaces)[dif].y;
-        const uint32_t w = eval_table(T, tt, src, dst, pkt_key(proto, dport));
-        if (COUNT) h.inc(w & 0x3FFFFFFFu);
-        return w;
+    }
+    // SYN: src interface inbound
+#pragma unroll
+    for (int j = 0; j < Q; j++) t[j] = es[j].tin, run[j] = live[j];
+    eval_step<Q, COUNT>(T, t, run, src, dst, ksyn, h, w);
+#pragma unroll
+    for (int j = 0; j < Q; j++) {
+        if (!run[j]) continue;
+        const uint32_t a = w[j] >> 30;
+        if (a == kActFailure || a == kActDeny) {
+            out[j] = verdict(a == kActFailure ? 3u : 0u, w[j] & kSlotMask);
+            live[j] = false;
+        } else if (a == kActReflect) {
+            srefl[j] = true;
+            drefl[j] = same[j];
+        }
+    }
+    // SYN: dst interface outbound
+#pragma unroll
+    for (int j = 0; j < Q; j++) t[j] = ed[j].tout, run[j] = live[j] && !drefl[j];
+    eval_step<Q, COUNT>(T, t, run, src, dst, ksyn, h, w);
+#pragma unroll
+    for (int j = 0; j < Q; j++) {
+        if (!run[j]) continue;
+        const uint32_t a = w[j] >> 30;
+        if (a == kActFailure || a == kActDeny) {
+            out[j] = verdict(a == kActFailure ? 3u : 0u, w[j] & kSlotMask);
+            live[j] = false;
+        } else if (a == kActReflect) {
+            drefl[j] = true;
+            if (same[j]) srefl[j] = true;
+        }
+    }
+    // SYN-ACK: dst interface inbound
+#pragma unroll
+    for (int j = 0; j < Q; j++) t[j] = ed[j].tin, run[j] = live[j] && !drefl[j];
+    eval_step<Q, COUNT>(T, t, run, dst, src, kack, h, w);
+#pragma unroll
+    for (int j = 0; j < Q; j++) {
+        if (!run[j]) continue;
+        const uint32_t a = w[j] >> 30;
+        if (a == kActFailure || a == kActDeny) {
+            out[j] = verdict(a == kActFailure ? 3u : 1u, w[j] & kSlotMask);
+            live[j] = false;
+        }
+    }
+    // SYN-ACK: src interface outbound
+#pragma unroll
+    for (int j = 0; j < Q; j++) t[j] = es[j].tout, run[j] = live[j] && !srefl[j];
+    eval_step<Q, COUNT>(T, t, run, dst, src, kack, h, w);
+#pragma unroll
+    for (int j = 0; j < Q; j++) {
+        if (!live[j]) continue;
+        const uint32_t a = w[j] >> 30;
+        if (run[j] && (a == kActFailure || a == kActDeny)) out[j] = verdict(a == kActFailure ? 3u : 1u, w[j] & kSlotMask);
+        else out[j] = verdict(2u, w[j] & kSlotMask);  // allowed; slot of the last evaluation
+    }
+}
+
+// Q tuples of one lane, any mode. SINGLE: tab0 is the (uniform) table, its blob at `blobs`.
+template <int MODE, bool COUNT, int Q>
+__device__ __forceinline__ void classify_q(const DevTableSet& T, const uint32_t* blobs, const DevTable& tab0,
+                                           const uint32_t (&s)[Q], const uint32_t (&d)[Q], const uint32_t (&sp)[Q],
+                                           const uint32_t (&dp)[Q], const uint32_t (&pr)[Q], const Hist& h,
+                                           uint32_t (&out)[Q]) {
+    uint32_t key[Q];
+#pragma unroll
+    for (int j = 0; j < Q; j++) key[j] = pkt_key(pr[j], dp[j]);
+    if (MODE == 0) {  // SINGLE
+        DevTable tab[Q];
+        bool act[Q];
+#pragma unroll
+        for (int j = 0; j < Q; j++) tab[j] = tab0, act[j] = true;
+        eval_q(T, blobs, tab, act, s, d, key, out);
+        if (COUNT) {
+#pragma unroll
+            for (int j = 0; j < Q; j++) h.inc(out[j] & kSlotMask);
+        }
+    } else if (MODE == 1) {  // PERPOD: outbound ACL of the interface dst is reached by
+        End e[Q];
+        probe_q(T, d, e);
+        int32_t t[Q];
+        bool run[Q];
+#pragma unroll
+        for (int j = 0; j < Q; j++) {
+            run[j] = e[j].ifc >= 0;
+            t[j] = e[j].tout;
+            if (!run[j]) {
+                out[j] = verdict(kActFailure, T.slot_unresolved);
+                if (COUNT) h.inc(T.slot_unresolved);
+            }
+        }
+        eval_step<Q, COUNT>(T, t, run, s, d, key, h, out);
     } else {  // CONN
-        const int32_t sif = iface_by_ip(T, src), dif = iface_by_ip(T, dst);
-        return test_connection<COUNT>(T, sif, dif, src, dst, pkt_key(proto, dport), pkt_key(proto, sport), h);
+        uint32_t ips[2 * Q];
+        End e[2 * Q];
+#pragma unroll
+        for (int j = 0; j < Q; j++) ips[j] = s[j], ips[Q + j] = d[j];
+        probe_q(T, ips, e);
+        End es[Q], ed[Q];
+        uint32_t kack[Q];
+#pragma unroll
+        for (int j = 0; j < Q; j++) es[j] = e[j], ed[j] = e[Q + j], kack[j] = pkt_key(pr[j], sp[j]);
+        conn_q<Q, COUNT>(T, es, ed, s, d, key, kack, h, out);
     }
 }
 
@@ -337,16 +451,15 @@ __global__ __launch_bounds__(kBlock) void k_classify(DevTableSet T, int32_t t, c
     uint32_t* hist = smem + (STAGE ? stage_words : 0u);
     Hist h{nullptr, counters};
     const bool use_lds = COUNT && T.n_slots <= kLdsHistMax;
-    Single sg{nullptr, BlobHdr{}, true};
+    DevTable tab0{};
+    const uint32_t* blobs = T.blobs;
     if (MODE == 0) {
-        const DevTable hd = T.tabs[t];
-        sg.linear = (hd.flags & kFlagLinear) != 0u;
+        tab0 = load_tab(T.tabs, t);
         if (STAGE) {
-            const uint4* g = reinterpret_cast<const uint4*>(T.blobs + hd.blob_off);
+            const uint4* g = reinterpret_cast<const uint4*>(T.blobs + tab0.blob_off);
             for (uint32_t i = threadIdx.x; i < stage_words / 4u; i += kBlock) reinterpret_cast<uint4*>(smem)[i] = g[i];
-            sg.b = smem;
-        } else {
-            sg.b = T.blobs + hd.blob_off;
+            blobs = smem;
+            tab0.blob_off = 0;
         }
     }
     if (COUNT && use_lds) {
@@ -354,7 +467,6 @@ __global__ __launch_bounds__(kBlock) void k_classify(DevTableSet T, int32_t t, c
         h.lds = hist;
     }
     if (STAGE || (COUNT && use_lds)) __syncthreads();
-    if (MODE == 0 && !sg.linear) sg.hdr = load_hdr(sg.b);
     const uint64_t stride = (uint64_t)gridDim.x * kBlock;
     const uint64_t first = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
     // full quads: software-pipelined -- the next quad's 44 bytes are in flight while this
@@ -382,22 +494,25 @@ __global__ __launch_bounds__(kBlock) void k_classify(DevTableSet T, int32_t t, c
         const uint64_t qn = q + stride;
         Quad nxt = cur;
         if (qn < nfull) nxt = load(qn);
-        v4u o;
-        o.x = classify_one<MODE, COUNT>(T, t, sg, cur.s.x, cur.d.x, cur.sp.x & 0xFFFFu, cur.dp.x & 0xFFFFu,
-                                        cur.pr & 0xFFu, h);
-        o.y = classify_one<MODE, COUNT>(T, t, sg, cur.s.y, cur.d.y, cur.sp.x >> 16, cur.dp.x >> 16,
-                                        (cur.pr >> 8) & 0xFFu, h);
-        o.z = classify_one<MODE, COUNT>(T, t, sg, cur.s.z, cur.d.z, cur.sp.y & 0xFFFFu, cur.dp.y & 0xFFFFu,
-                                        (cur.pr >> 16) & 0xFFu, h);
-        o.w = classify_one<MODE, COUNT>(T, t, sg, cur.s.w, cur.d.w, cur.sp.y >> 16, cur.dp.y >> 16, cur.pr >> 24, h);
-        stream_store(o, reinterpret_cast<v4u*>(out + (q << 2)));
+        const uint32_t s4[4] = {cur.s.x, cur.s.y, cur.s.z, cur.s.w};
+        const uint32_t d4[4] = {cur.d.x, cur.d.y, cur.d.z, cur.d.w};
+        const uint32_t dp4[4] = {cur.dp.x & 0xFFFFu, cur.dp.x >> 16, cur.dp.y & 0xFFFFu, cur.dp.y >> 16};
+        const uint32_t sp4[4] = {cur.sp.x & 0xFFFFu, cur.sp.x >> 16, cur.sp.y & 0xFFFFu, cur.sp.y >> 16};
+        const uint32_t pr4[4] = {cur.pr & 0xFFu, (cur.pr >> 8) & 0xFFu, (cur.pr >> 16) & 0xFFu, cur.pr >> 24};
+        uint32_t o[4];
+        classify_q<MODE, COUNT, 4>(T, blobs, tab0, s4, d4, sp4, dp4, pr4, h, o);
+        stream_store(v4u{o[0], o[1], o[2], o[3]}, reinterpret_cast<v4u*>(out + (q << 2)));
         cur = nxt;
         q = qn;
     }
     // remainder (or everything when the pointers are not vector-aligned): one tuple per lane
-    for (uint64_t i = (nfull << 2) + first; i < n; i += stride)
-        out[i] = classify_one<MODE, COUNT>(T, t, sg, src[i], dst[i], MODE == 2 ? sport[i] : 0u, dport[i], proto[i],
-                                           h);
+    for (uint64_t i = (nfull << 2) + first; i < n; i += stride) {
+        const uint32_t s1[1] = {src[i]}, d1[1] = {dst[i]}, sp1[1] = {MODE == 2 ? (uint32_t)sport[i] : 0u},
+                       dp1[1] = {dport[i]}, pr1[1] = {proto[i]};
+        uint32_t o[1];
+        classify_q<MODE, COUNT, 1>(T, blobs, tab0, s1, d1, sp1, dp1, pr1, h, o);
+        out[i] = o[0];
+    }
     if (COUNT && use_lds) {
         __syncthreads();
         for (uint32_t i = threadIdx.x; i < T.n_slots; i += kBlock) {
@@ -517,24 +632,56 @@ __global__ void k_conn_queries(DevTableSet T, const ConnQueryDev* q, uint32_t n,
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const ConnQueryDev c = q[i];
-    Hist h{nullptr, nullptr};
-    out[i] = test_connection<false>(T, c.src_if, c.dst_if, c.src_ip, c.dst_ip, c.key_syn, c.key_synack, h);
+    auto end = [&](int32_t ifc) {
+        return ifc < 0 ? End{-1, -1, -1} : End{ifc, T.ifaces[2 * ifc], T.ifaces[2 * ifc + 1]};
+    };
+    const End es[1] = {end(c.src_if)}, ed[1] = {end(c.dst_if)};
+    const uint32_t s1[1] = {c.src_ip}, d1[1] = {c.dst_ip}, ks[1] = {c.key_syn}, ka[1] = {c.key_synack};
+    uint32_t o[1];
+    conn_q<1, false>(T, es, ed, s1, d1, ks, ka, Hist{nullptr, nullptr}, o);
+    out[i] = o[0];
 }
 
 // ---- launchers --------------------------------------------------------------------------------
-static uint32_t g_blocks_per_cu = 4;        // grid = min(work, 256 CUs x this), grid-stride beyond
+static uint32_t g_blocks_per_cu = 0;        // 0: as many workgroups per CU as fit (occupancy)
 static uint32_t g_stage_max_words = 16384;  // blobs up to 64 KiB are staged in LDS
 
 int dev_set_tuning(const std::string& key, int value) {
-    if (key == "blocks_per_cu" && value > 0 && value <= 64) g_blocks_per_cu = (uint32_t)value;
+    if (key == "blocks_per_cu" && value >= 0 && value <= 64) g_blocks_per_cu = (uint32_t)value;
     else if (key == "stage_max_words" && value >= 0 && value <= 36864) g_stage_max_words = (uint32_t)value;
     else return -1;
     return 0;
 }
 
+static uint32_t num_cus() {
+    static int cached_dev = -1;
+    static uint32_t cus = 256;
+    int dev = 0;
+    if (hipGetDevice(&dev) == hipSuccess && dev != cached_dev) {
+        hipDeviceProp_t p;
+        if (hipGetDeviceProperties(&p, dev) == hipSuccess && p.multiProcessorCount > 0) cus = p.multiProcessorCount;
+        cached_dev = dev;
+    }
+    return cus;
+}
+
 static int grid_for(uint64_t items) {
+    const uint32_t bpc = g_blocks_per_cu ? g_blocks_per_cu : 4u;
     uint64_t g = (items + kBlock - 1) / kBlock;
-    return (int)std::max<uint64_t>(1, std::min<uint64_t>(g, 256ull * g_blocks_per_cu));
+    return (int)std::max<uint64_t>(1, std::min<uint64_t>(g, (uint64_t)num_cus() * bpc));
+}
+
+// Grid of a grid-stride classify kernel: exactly the workgroups that are resident at once
+// (registers / LDS of this instantiation), so no workgroup waits for another to finish, capped
+// by the work and by blocks_per_cu when set.
+template <class K>
+static int grid_resident(K kernel, size_t lds, uint64_t items) {
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kBlock, lds) != hipSuccess || per_cu < 1)
+        per_cu = 1;
+    if (g_blocks_per_cu) per_cu = std::min<int>(per_cu, (int)g_blocks_per_cu);
+    const uint64_t g = (items + kBlock - 1) / kBlock;
+    return (int)std::max<uint64_t>(1, std::min<uint64_t>(g, (uint64_t)num_cus() * per_cu));
 }
 
 template <int MODE, bool COUNT, bool VEC>
@@ -545,15 +692,20 @@ static void launch_classify(const DevTableSet& T, int t, const uint32_t* src, co
     uint32_t stage = 0;
     if (MODE == 0) {
         const DevTable& hd = T.host_tabs[t];
-        if (!(hd.flags & kFlagLinear) && hd.blob_words <= g_stage_max_words) stage = hd.blob_words;
+        const uint32_t words = T.host_blob_words[t];
+        if (!(hd.fsk & kFlagLinear) && words <= g_stage_max_words) stage = words;
     }
-    const dim3 grid(grid_for((n + 3) / 4));
-    if (stage)
-        hipLaunchKernelGGL((k_classify<MODE, COUNT, VEC, true>), grid, dim3(kBlock), hist + stage * 4, st, T, t, src,
-                           dst, sport, dport, proto, n, out, counters, stage);
-    else
-        hipLaunchKernelGGL((k_classify<MODE, COUNT, VEC, false>), grid, dim3(kBlock), hist, st, T, t, src, dst, sport,
+    const uint64_t items = VEC ? (n + 3) / 4 : n;
+    if (stage) {
+        auto k = k_classify<MODE, COUNT, VEC, true>;
+        const size_t lds = hist + stage * 4;
+        hipLaunchKernelGGL(k, dim3(grid_resident(k, lds, items)), dim3(kBlock), lds, st, T, t, src, dst, sport, dport,
+                           proto, n, out, counters, stage);
+    } else {
+        auto k = k_classify<MODE, COUNT, VEC, false>;
+        hipLaunchKernelGGL(k, dim3(grid_resident(k, hist, items)), dim3(kBlock), hist, st, T, t, src, dst, sport,
                            dport, proto, n, out, counters, 0u);
+    }
 }
 
 template <int MODE>

@@ -4,10 +4,11 @@
 // Layout in HBM (one "table set"; a new set is uploaded and swapped in on every change):
 //   rules   DevRule[NR]   all ACLs' rules concatenated, ACL order preserved (linear kernel,
 //                         ANY-protocol packets, generator)
-//   tabs    DevTable[T]   per-ACL header
+//   tabs    DevTable[T]   per-ACL header incl. everything the blob walk needs (one 32-B read)
 //   blobs   u32[]         per-ACL classification blob (fastpath.cpp), 16-byte aligned
 //   ifaces  int2[NI]      per interface {inbound table, outbound table} (-1 = no ACL)
-//   iphash  uint2[cap]    IPv4 -> interface (open addressing, EMPTY = 0xFFFFFFFF value)
+//   iphash  uint4[cap]    IPv4 -> {ip, interface, inbound table, outbound table} of a local
+//                         pod (open addressing; EMPTY: interface = 0xFFFFFFFF)
 #pragma once
 #include <cstdint>
 #include <string>
@@ -28,13 +29,15 @@ struct DevRule {           // 32 B, one compiled vpp_acl rule
     uint32_t pad;
 };
 
-struct DevTable {          // 32 B
+struct DevTable {          // 32 B: two 16-B loads
+    uint32_t blob_off;     // in u32 words, multiple of 4
+    uint32_t fsk;          // flags (blob[0]; 8 = linear) | s1 << 8 | k1 << 16
+    uint32_t dflt;         // default verdict: DENY << 30 | default slot
+    uint32_t kroot;        // blob[4]
+    uint32_t xoff;         // blob[6]
+    uint32_t nkc;          // blob[7]
     uint32_t rule_base;    // first rule (global index == counter slot)
     uint32_t n_rules;
-    uint32_t blob_off;     // in u32 words, multiple of 4
-    uint32_t blob_words;
-    uint32_t flags;        // copy of blob[0]
-    uint32_t pad[3];
 };
 
 struct DevTableSet {       // device pointers (valid on the GPU)
@@ -42,27 +45,30 @@ struct DevTableSet {       // device pointers (valid on the GPU)
     const DevTable* tabs;
     const uint32_t* blobs;
     const int32_t* ifaces; // int2 pairs
-    const uint32_t* iphash;// uint2 pairs {ip, iface}
+    const uint32_t* iphash;// uint4 {ip, iface, in table, out table}
     uint32_t iphash_mask;
     int32_t node_if;       // interface of non-local IPs, -1 = none (FAILURE)
+    int32_t node_in, node_out;  // its ACL tables (-1 = none)
     uint32_t n_rules;      // NR
     uint32_t n_tables;     // T
     uint32_t n_ifaces;
     uint32_t slot_noacl;   // NR + T
     uint32_t slot_unresolved;
     uint32_t n_slots;
-    const DevTable* host_tabs;  // host copy of tabs (launch decisions; not dereferenced on the GPU)
+    const DevTable* host_tabs;       // host copies (launch decisions; not dereferenced on the GPU)
+    const uint32_t* host_blob_words;
 };
 
 // Host image of a table set, produced by the compiler and uploaded as one blob.
 struct HostTableSet {
     std::vector<DevRule> rules;
     std::vector<DevTable> tabs;
+    std::vector<uint32_t> blob_words;  // per table (0 = linear)
     std::vector<uint32_t> blobs;
     std::vector<int32_t> ifaces;
     std::vector<uint32_t> iphash;
     uint32_t iphash_mask = 0;
-    int32_t node_if = -1;
+    int32_t node_if = -1, node_in = -1, node_out = -1;
 };
 
 // fastpath.cpp: classification blob of one table (false = does not fit the budgets)

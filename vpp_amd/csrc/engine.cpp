@@ -1,6 +1,8 @@
 // Device ACL engine: ACL install semantics + the table compiler.
 #include "engine.hpp"
 
+#include "blobwalk.hpp"
+
 #include <algorithm>
 #include <set>
 
@@ -209,19 +211,23 @@ void Engine::compile() {
         h.tabs.push_back(hdr);
     }
     const uint32_t NR = (uint32_t)h.rules.size();
+    h.blob_words.assign(h.tabs.size(), 0);
     for (size_t t = 0; t < h.tabs.size(); t++) {
         DevTable& hdr = h.tabs[t];
         std::vector<uint32_t> blob;
-        hdr.blob_off = (uint32_t)h.blobs.size();
+        hdr.dflt = (kActDeny << 30) | (NR + (uint32_t)t);
         if (build_fast_table(h.rules.data() + hdr.rule_base, hdr.n_rules, hdr.rule_base, NR + (uint32_t)t, blob,
                              1ull << 22)) {
             while (blob.size() % 4) blob.push_back(0);
-            hdr.flags = blob[0];
-            hdr.blob_words = (uint32_t)blob.size();
+            hdr.blob_off = (uint32_t)h.blobs.size();
+            hdr.fsk = blob[0] | (blob[3] << 8) | (blob[5] << 16);
+            hdr.kroot = blob[4];
+            hdr.xoff = blob[6];
+            hdr.nkc = blob[7];
+            h.blob_words[t] = (uint32_t)blob.size();
             h.blobs.insert(h.blobs.end(), blob.begin(), blob.end());
         } else {
-            hdr.flags = 8;  // linear scan fallback
-            hdr.blob_words = 0;
+            hdr.fsk = kFlagLinear;  // linear scan fallback
         }
     }
     uint32_t T = (uint32_t)h.tabs.size();
@@ -245,24 +251,37 @@ void Engine::compile() {
     }
     std::string nif = node_if_name();
     h.node_if = nif.empty() ? -1 : iface_index[nif];
-    // local pod IP -> TAP interface
-    std::vector<std::pair<uint32_t, int32_t>> ipmap;
+    if (h.node_if >= 0) h.node_in = h.ifaces[2 * h.node_if], h.node_out = h.ifaces[2 * h.node_if + 1];
+    // local pod IP -> {TAP interface, its inbound / outbound tables}; -2 = pod without a
+    // known interface (unresolvable, FAILURE)
+    struct Ent {
+        uint32_t ip;
+        int32_t ifc, tin, tout;
+    };
+    std::vector<Ent> ipmap;
     for (auto& kv : pods) {
         Bytes v4;
         if (kv.second.another_node || !to4(kv.second.ip, &v4)) continue;
         std::string ifn;
-        int32_t idx = ifaces.if_name(kv.first, &ifn) ? iface_index[ifn] : -2;
-        ipmap.push_back({ipv4_u32(v4), idx});
+        Ent e{ipv4_u32(v4), -2, -1, -1};
+        if (ifaces.if_name(kv.first, &ifn)) {
+            e.ifc = iface_index[ifn];
+            e.tin = h.ifaces[2 * e.ifc];
+            e.tout = h.ifaces[2 * e.ifc + 1];
+        }
+        ipmap.push_back(e);
     }
     uint32_t cap = 16;
     while (cap < 2 * ipmap.size() + 16) cap <<= 1;
-    h.iphash.assign(2 * cap, 0xFFFFFFFFu);
+    h.iphash.assign(4 * cap, 0xFFFFFFFFu);
     h.iphash_mask = cap - 1;
     for (auto& e : ipmap) {
-        uint32_t s = hash_ip(e.first) & h.iphash_mask;
-        while (h.iphash[2 * s + 1] != 0xFFFFFFFFu && h.iphash[2 * s] != e.first) s = (s + 1) & h.iphash_mask;
-        h.iphash[2 * s] = e.first;
-        h.iphash[2 * s + 1] = (uint32_t)e.second;
+        uint32_t s = hash_ip(e.ip) & h.iphash_mask;
+        while (h.iphash[4 * s + 1] != 0xFFFFFFFFu && h.iphash[4 * s] != e.ip) s = (s + 1) & h.iphash_mask;
+        h.iphash[4 * s] = e.ip;
+        h.iphash[4 * s + 1] = (uint32_t)e.ifc;
+        h.iphash[4 * s + 2] = (uint32_t)e.tin;
+        h.iphash[4 * s + 3] = (uint32_t)e.tout;
     }
     compiled = true;
 }

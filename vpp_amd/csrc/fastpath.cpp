@@ -9,8 +9,9 @@
 //   CROSS mode:  cross[src class][key class] -> verdict of the first rule whose src and L4
 //                match and whose dst is ANY, plus (LISTS) the short ordered list of
 //                dst-specific rules in front of it, tested on dst only.
-//   CAND mode:   (tables too large for a cross product) src class -> ordered candidate list
-//                of rules whose src matches, tested on dst + L4 key.
+//   CAND mode:   (tables too large for a cross product) the src trie's leaf is the first
+//                record of the class's ordered candidate list (rules whose src matches),
+//                tested on dst + L4 key.
 //
 // src classes = equivalence classes of the elementary src intervals (cut at every rule's
 // prefix boundary) by the ordered list of rules whose src covers them, truncated after the
@@ -24,14 +25,18 @@
 // copied verbatim into LDS:
 //   [0]  flags: 1 = CROSS, 2 = LISTS, 4 = CAND
 //   [1]  default verdict (DENY << 30 | table's default slot)
-//   [2]  src trie root   [3] s1     [4] key trie root   [5] k1
-//   [6]  cross / class-table offset [7] n_key_classes   [8] list / candidate offset
-//   [9]  candidate verdict offset   [10] n_src_classes  [11..15] reserved
+//   [2]  src trie root (always 16)   [3] s1     [4] key trie root   [5] k1
+//   [6]  CROSS: cross table (u32 verdicts, or LISTS: u2 {verdict, first record | 0});
+//        CAND: first record
+//   [7]  n_key_classes   [10] n_src_classes   [8, 9, 11..15] reserved
+//   records (16 B, blobwalk.hpp): {dnet, klo | dst prefix length << 18, khi, verdict}; every
+//   list ends with a match-all record carrying the fall-through verdict.
 #include <algorithm>
 #include <map>
 #include <set>
 #include <unordered_map>
 
+#include "blobwalk.hpp"
 #include "engine.hpp"
 
 namespace pg {
@@ -116,6 +121,23 @@ bool build_fast_table(const DevRule* rules, uint32_t n, uint32_t rule_base, uint
     const uint32_t dflt = (kActDeny << 30) | default_slot;
     blob[1] = dflt;
     auto verdict = [&](uint32_t i) { return ((rules[i].act & 3u) << 30) | (rule_base + i); };
+    // records test the dst as a prefix length: every compiled dst mask is a CIDR mask
+    auto dlen = [](uint32_t m, uint32_t* len) {
+        uint32_t l = (uint32_t)__builtin_popcount(m);
+        if (rec_mask(l) != m) return false;
+        *len = l;
+        return true;
+    };
+    for (uint32_t i = 0; i < n; i++) {
+        uint32_t l = 0;
+        if (live(rules[i]) && !dlen(rules[i].dmask, &l)) return false;
+    }
+    auto put_rec = [&](uint32_t dnet, uint32_t dl, uint32_t klo, uint32_t khi, uint32_t v) {
+        blob.push_back(dnet);
+        blob.push_back(klo | (dl << 18));
+        blob.push_back(khi);
+        blob.push_back(v);
+    };
 
     // ---- src: elementary intervals and their candidate lists ------------------------------
     std::vector<uint64_t> sb{0};
@@ -159,23 +181,23 @@ bool build_fast_table(const DevRule* rules, uint32_t n, uint32_t rule_base, uint
         auto it = src_cls_of.find(lst);
         if (it == src_cls_of.end()) {
             it = src_cls_of.emplace(lst, (uint32_t)src_lists.size()).first;
-            total_cand += lst.size();
+            total_cand += lst.size() + 1;
             src_lists.push_back(lst);
             if (total_cand > (1ull << 26)) return false;
         }
         sint_cls[k] = it->second;
     }
     const uint32_t nsc = (uint32_t)src_lists.size();
-    uint32_t s1 = pick_stride(sb.size(), 32);
-    blob[2] = build_trie(blob, sb, sint_cls, 32, s1);
-    blob[3] = s1;
     blob[10] = nsc;
 
-    // ---- try the cross product ---------------------------------------------------------
+    // ---- key classes and the cross product, if it fits ---------------------------------------
     bool cross = n <= 16384;
     std::vector<uint64_t> kb{0};
     std::vector<uint32_t> kseg_cls;
     std::vector<std::vector<uint32_t>> key_sets;  // sorted rule indices covering the segment
+    std::vector<uint32_t> cverd;
+    std::vector<std::vector<uint32_t>> clist;
+    bool lists = false;
     if (cross) {
         for (uint32_t i = 0; i < n; i++) {
             if (!live(rules[i])) continue;
@@ -209,90 +231,99 @@ bool build_fast_table(const DevRule* rules, uint32_t n, uint32_t rule_base, uint
         }
         if ((uint64_t)nsc * key_sets.size() > cross_budget) cross = false;
     }
-
     if (cross) {
+        // first rule of (src class list) covering the key class; dst-specific rules in front
+        // of it form the class pair's dst list
         const uint32_t nkc = (uint32_t)key_sets.size();
-        uint32_t k1 = pick_stride(kb.size(), 18);
-        blob[4] = build_trie(blob, kb, kseg_cls, 18, k1);
-        blob[5] = k1;
-        blob[7] = nkc;
-        // membership bitsets of key classes
         const size_t words = (n + 63) / 64;
         std::vector<uint64_t> kbits((size_t)nkc * words, 0);
         for (uint32_t c = 0; c < nkc; c++)
             for (uint32_t r : key_sets[c]) kbits[(size_t)c * words + r / 64] |= 1ull << (r % 64);
-        std::vector<uint32_t> cverd((size_t)nsc * nkc);
-        std::vector<std::vector<uint32_t>> clist((size_t)nsc * nkc);
-        bool lists = false;
-        for (uint32_t s = 0; s < nsc; s++) {
+        cverd.assign((size_t)nsc * nkc, dflt);
+        clist.assign((size_t)nsc * nkc, {});
+        for (uint32_t s = 0; s < nsc && cross; s++) {
             for (uint32_t c = 0; c < nkc; c++) {
                 const uint64_t* bits = &kbits[(size_t)c * words];
-                uint32_t v = dflt;
                 std::vector<uint32_t>& L = clist[(size_t)s * nkc + c];
                 for (uint32_t r : src_lists[s]) {
                     if (!((bits[r / 64] >> (r % 64)) & 1)) continue;
                     if (rules[r].dmask == 0) {
-                        v = verdict(r);
+                        cverd[(size_t)s * nkc + c] = verdict(r);
                         break;
                     }
                     L.push_back(r);
                 }
-                if (L.size() > 255) return build_fast_table(rules, n, rule_base, default_slot, blob, 0);
+                if (L.size() > 255) {  // long dst lists: the candidate form is as good
+                    cross = false;
+                    break;
+                }
                 if (!L.empty()) lists = true;
-                cverd[(size_t)s * nkc + c] = v;
             }
         }
+    }
+
+    if (cross) {
+        const uint32_t nkc = (uint32_t)key_sets.size();
+        const uint32_t s1 = pick_stride(sb.size(), 32);
+        if (build_trie(blob, sb, sint_cls, 32, s1) != kSrcRoot) return false;
+        blob[2] = kSrcRoot;
+        blob[3] = s1;
+        const uint32_t k1 = pick_stride(kb.size(), 18);
+        blob[4] = build_trie(blob, kb, kseg_cls, 18, k1);
+        blob[5] = k1;
+        blob[7] = nkc;
         while (blob.size() % 4) blob.push_back(0);
         blob[6] = (uint32_t)blob.size();
         if (!lists) {
-            blob[0] = 1;
+            blob[0] = kFlagCross;
             blob.insert(blob.end(), cverd.begin(), cverd.end());
-        } else {
-            blob[0] = 1 | 2;
-            size_t xoff = blob.size();
-            blob.resize(blob.size() + 2 * cverd.size(), 0);
-            for (size_t e = 0; e < cverd.size(); e++) {
-                blob[xoff + 2 * e] = cverd[e];
-                const auto& L = clist[e];
-                if (L.empty()) continue;
-                while (blob.size() % 4) blob.push_back(0);
-                uint32_t loff = (uint32_t)blob.size();
-                if (loff >= (1u << 24)) return build_fast_table(rules, n, rule_base, default_slot, blob, 0);
-                for (uint32_t r : L) {
-                    blob.push_back(rules[r].dnet);
-                    blob.push_back(rules[r].dmask);
-                    blob.push_back(verdict(r));
-                    blob.push_back(0);
-                }
-                blob[xoff + 2 * e + 1] = (loff << 8) | (uint32_t)L.size();
+            return true;
+        }
+        blob[0] = kFlagCross | kFlagLists;
+        const size_t xoff = blob.size();
+        blob.resize(blob.size() + 2 * cverd.size(), 0);
+        while (blob.size() % 4) blob.push_back(0);
+        for (size_t e = 0; e < cverd.size(); e++) {
+            blob[xoff + 2 * e] = cverd[e];
+            const auto& L = clist[e];
+            if (L.empty()) continue;
+            if (blob.size() >= 0x7FFFFFF0u) return false;
+            blob[xoff + 2 * e + 1] = (uint32_t)blob.size();
+            for (uint32_t r : L) {
+                uint32_t l = 0;
+                dlen(rules[r].dmask, &l);
+                put_rec(rules[r].dnet, l, 0, kKeyMax, verdict(r));  // key already covered by the class
             }
+            put_rec(0, 0, 0, kKeyMax, cverd[e]);  // fall through to the pair's verdict
         }
         return true;
     }
 
-    // ---- candidate mode -------------------------------------------------------------------
-    blob[0] = 4;
-    while (blob.size() % 4) blob.push_back(0);
-    blob[6] = (uint32_t)blob.size();  // per src class {cand offset (in entries), count}
-    size_t coff = blob.size();
-    blob.resize(blob.size() + 2 * (size_t)nsc, 0);
-    std::vector<uint32_t> cand, cverd;
+    // ---- candidate mode: src trie leaves point at the class's record list -------------------
+    std::vector<uint32_t> first_rec(nsc);
+    uint64_t nrec = 0;
     for (uint32_t s = 0; s < nsc; s++) {
-        blob[coff + 2 * s] = (uint32_t)(cverd.size());
-        blob[coff + 2 * s + 1] = (uint32_t)src_lists[s].size();
-        for (uint32_t r : src_lists[s]) {
-            cand.push_back(rules[r].dnet);
-            cand.push_back(rules[r].dmask);
-            cand.push_back(rules[r].klo);
-            cand.push_back(rules[r].khi);
-            cverd.push_back(verdict(r));
-        }
+        first_rec[s] = (uint32_t)nrec;
+        nrec += src_lists[s].size() + 1;
     }
-    while (blob.size() % 4) blob.push_back(0);  // uint4 alignment of the candidate array
-    blob[8] = (uint32_t)blob.size();
-    blob.insert(blob.end(), cand.begin(), cand.end());
-    blob[9] = (uint32_t)blob.size();
-    blob.insert(blob.end(), cverd.begin(), cverd.end());
+    if (nrec >= (1ull << 29)) return false;
+    std::vector<uint32_t> leaf(sb.size());
+    for (size_t k = 0; k < sb.size(); k++) leaf[k] = first_rec[sint_cls[k]];
+    const uint32_t s1 = pick_stride(sb.size(), 32);
+    if (build_trie(blob, sb, leaf, 32, s1) != kSrcRoot) return false;
+    blob[0] = kFlagCand;
+    blob[2] = kSrcRoot;
+    blob[3] = s1;
+    while (blob.size() % 4) blob.push_back(0);  // 16-byte records
+    blob[6] = (uint32_t)blob.size();
+    for (uint32_t s = 0; s < nsc; s++) {
+        for (uint32_t r : src_lists[s]) {
+            uint32_t l = 0;
+            dlen(rules[r].dmask, &l);
+            put_rec(rules[r].dnet, l, rules[r].klo, rules[r].khi, verdict(r));
+        }
+        put_rec(0, 0, 0, kKeyMax, dflt);  // no candidate matched: the table's default deny
+    }
     return true;
 }
 
