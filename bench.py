@@ -23,6 +23,7 @@ import torch.distributed as dist
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+from vpp_amd import _capi  # noqa: E402
 from vpp_amd import device as D  # noqa: E402
 from vpp_amd import dist as VD  # noqa: E402
 from vpp_amd import workloads as W  # noqa: E402
@@ -43,6 +44,8 @@ def parse():
     p.add_argument("--counters", action="store_true", help="time with per-rule hit counters on")
     p.add_argument("--cpu-sample", type=int, default=4 << 20, help="tuples in the CPU-baseline sample")
     p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--per-table", action="store_true",
+                   help="PERPOD/CONN through the per-table blobs + IP hash instead of the node classifier")
     return p.parse_args()
 
 
@@ -55,6 +58,8 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     else:
         torch.cuda.set_device(local)
+    if a.per_table:
+        assert _capi.lib.pg_set_tuning(b"node_path", 0) == 0
     kw = {"n_tuples": a.tuples} if a.tuples else {}
     w = W.CONFIGS[a.config](local, **kw)
     e, n = w.engine, w.n_tuples
@@ -115,7 +120,7 @@ def main():
         "vs_baseline": None, "dtype": "u32", "data": "synthetic (device-generated, counter-based splitmix64)",
         "config": {"workload": "config%d: %s" % (a.config, w.desc), "mode": MODE_NAME[w.mode],
                    "tuples_per_gpu": n, "rules": st["rules"], "tables": st["tables"], "parallelism": "dp%d" % world,
-                   "counters": bool(use_counters)},
+                   "counters": bool(use_counters), "classifier": classifier(w, a.per_table)},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "bytes_per_tuple": BYTES_PER_TUPLE[w.mode], "kernel_ms": round(kern_ms, 4),
@@ -129,6 +134,17 @@ def main():
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def classifier(w, per_table):
+    """the structure the timed kernel walks"""
+    e = w.engine
+    if w.mode == 0:
+        return "table blob: %s" % json.dumps(e.table_stats(w.table_id))
+    ns = None if per_table else e.node_stats()
+    if ns is None:
+        return "per-table blobs + IPv4 hash"
+    return "node: %s" % json.dumps(ns)
 
 
 def pmc_traffic(config, n, counters):

@@ -139,7 +139,12 @@ pg_ctx* pg_create(int hip_device);
  * grid; default 0 = as many as registers/LDS allow),
  * "stage_max_words" (largest table blob staged in LDS, default 16384 = 64 KiB),
  * "root_bits_max" (cap of the src/key trie root stride, 4..16, default 16; affects tables
- * compiled afterwards) */
+ * compiled afterwards),
+ * "node_build" (1/0: build the node classifier for PERPOD / CONN, default 1; tables compiled
+ * afterwards), "node_root_bits" (its IPv4 / key trie root stride cap, default 12),
+ * "node_path" (1/0: classify PERPOD / CONN through the node classifier when it exists,
+ * default 1; 0 = per-table blobs and the IP hash), "node_stage_max_words" (largest node
+ * image staged in LDS, default 16384) */
 int pg_set_tuning(const char* key, int value);
 void pg_destroy(pg_ctx* ctx);
 const char* pg_last_error(const pg_ctx* ctx);
@@ -201,6 +206,16 @@ int pg_classify(pg_ctx* ctx, int mode, int table_id, const pg_tuple_soa* tuples,
  * compiler can be checked against the oracle without a GPU. Does not touch the device. */
 int pg_debug_walk_blob(pg_ctx* ctx, const char* acl_name, const uint32_t* src, const uint32_t* dst,
                        const uint16_t* dst_port, const uint8_t* proto, uint64_t n, uint32_t* out);
+/* TESTS ONLY -- never on the classify path: pg_classify's per-tuple code (classify.hpp, the
+ * same templates the kernels instantiate) run on the host over host tuples, any mode, with
+ * optional host u64 counters; node = 1 uses the node classifier when it exists, 0 the
+ * per-table path. Does not touch the device. */
+int pg_debug_classify_host(pg_ctx* ctx, int mode, int table_id, const pg_tuple_soa* tuples, uint64_t n,
+                           uint32_t* out, uint64_t* counters, int node);
+/* node classifier (PERPOD / CONN) size: IPv4 classes, L4-key classes, LDS image bytes,
+ * cross-table bytes; PG_ENOENT when it was not built */
+int pg_node_stats(pg_ctx* ctx, uint32_t* ip_classes, uint32_t* key_classes, uint64_t* image_bytes,
+                  uint64_t* cross_bytes);
 /* reference-shaped linear-scan kernel (K1) on one table, for validation and comparison */
 int pg_classify_linear(pg_ctx* ctx, int table_id, const pg_tuple_soa* tuples, uint64_t n, uint32_t* out,
                        void* hip_stream);

@@ -74,7 +74,7 @@ class OraACL:
         self.h = lib.ora_acl_new(self.arr, self.n)
 
     def __del__(self):
-        if getattr(self, "h", None):
+        if getattr(self, "h", None) and lib is not None:  # lib is None at interpreter shutdown
             lib.ora_acl_free(self.h)
             self.h = None
 

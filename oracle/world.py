@@ -13,8 +13,10 @@ from . import fast
 
 
 class World:
-    def __init__(self, engine, local_ifs, node_if):
-        """local_ifs: {IPv4 u32: TAP name} of the pods on this node; node_if: name or None."""
+    def __init__(self, engine, local_ifs, node_if, no_if_ips=()):
+        """local_ifs: {IPv4 u32: TAP name} of the pods on this node; node_if: name or None;
+        no_if_ips: IPv4s of pods on this node whose interface is unknown (unresolvable:
+        "Missing interface for ... pod", aclengine_mock.go:302-306 -> FAILURE)."""
         self.names = engine.ACLNames()
         self.acls = [fast.OraACL(engine.GetACLByName(n)["rules"]) for n in self.names]
         tix = {n: i for i, n in enumerate(self.names)}
@@ -23,9 +25,9 @@ class World:
         bind = [engine._if_acls(x) for x in ifnames]
         self.if_in = np.array([tix.get(b[0], -1) for b in bind], np.int32)
         self.if_out = np.array([tix.get(b[1], -1) for b in bind], np.int32)
-        ips = sorted(local_ifs)
+        ips = sorted(set(local_ifs) | set(no_if_ips))
         self.local_ips = np.array(ips, np.uint32)
-        self.local_if = np.array([self.ifx[local_ifs[ip]] for ip in ips], np.int32)
+        self.local_if = np.array([self.ifx[local_ifs[ip]] if ip in local_ifs else -1 for ip in ips], np.int32)
         self.node = self.ifx[node_if] if node_if else -1
         # slot layout of the engine (pg_table_info / pg_num_counter_slots)
         info = [engine.table_info(engine.table_id(n)) for n in self.names]

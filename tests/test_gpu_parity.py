@@ -197,7 +197,7 @@ def test_conn_and_perpod_modes_random_topology(seed):
     names, ora, tid = _oracle_world(e, acls)
     assert [e.table_id(n) for n in names] == list(range(len(names)))
     pod_ips = [fz_ip(p[1]) for p in pods]
-    n = 60000
+    n = 60001 + seed  # ragged: the one-tuple tail loop too
     rng = np.random.default_rng(seed)
     tup = list(fz.rand_tuples(rng, n, fz.ANCHORS + pod_ips))
     for k in (0, 1):  # 60 % of endpoints are pods
@@ -284,3 +284,38 @@ def test_cluster_configs_gpu_vs_oracle(config):
     assert ((got >> 30) == act.astype(np.uint32)).all()
     assert ((got & 0x3FFFFFFF) == slot).all()
     assert len(np.unique(got >> 30)) >= 2
+
+
+def _classify_with(e, mode, b, node_path, stage_words=16384, counters=False):
+    lib = R.lib
+    assert lib.pg_set_tuning(b"node_path", node_path) == 0
+    assert lib.pg_set_tuning(b"node_stage_max_words", stage_words) == 0
+    try:
+        out = torch.empty(b.n, dtype=torch.int32, device="cuda")
+        cnt = torch.zeros(e.num_counter_slots(), dtype=torch.int64, device="cuda") if counters else None
+        D.classify(e, mode, -1, b, out, counters=cnt)
+        torch.cuda.synchronize()
+        return out.cpu().numpy().view(np.uint32), (cnt.cpu().numpy() if counters else None)
+    finally:
+        lib.pg_set_tuning(b"node_path", 1)
+        lib.pg_set_tuning(b"node_stage_max_words", 16384)
+
+
+@pytest.mark.parametrize("config", [3, 5])
+def test_node_kernel_equals_per_table_kernel(config):
+    """The node classifier (LDS-staged and read from HBM) and the per-table blobs + IPv4 hash
+    give identical verdicts and hit counters on the cluster configs, and both equal the
+    host run of the same per-tuple code (pg_debug_classify_host) on a ragged batch."""
+    from vpp_amd import workloads as W
+    w = W.CONFIGS[config](0, n_tuples=(1 << 20) + 3)
+    e = w.engine
+    assert e.node_stats() is not None
+    b = D.TupleBatch(w.n_tuples, with_sport=True)
+    D.gen_tuples(e, b, **w.gen)
+    staged, c1 = _classify_with(e, w.mode, b, 1, counters=True)
+    hbm, c2 = _classify_with(e, w.mode, b, 1, stage_words=0, counters=True)
+    table, c3 = _classify_with(e, w.mode, b, 0, counters=True)
+    assert np.array_equal(staged, hbm) and np.array_equal(staged, table)
+    assert np.array_equal(c1, c2) and np.array_equal(c1, c3)
+    host = e.debug_classify_host(w.mode, -1, *b.numpy(b.n), node=True)
+    assert np.array_equal(host, staged)

@@ -1,0 +1,166 @@
+"""The node classifier (fastpath.cpp build_node; PERPOD / CONN modes) checked on the host.
+
+pg_debug_classify_host runs pg_classify's per-tuple code (vpp_amd/csrc/classify.hpp, the
+templates the kernels instantiate) on the CPU. For every topology below the node path, the
+per-table path (per-ACL blobs + IPv4 hash) and the C oracle's evalACL / testConnection
+(oracle.world over the engine's exported ACLs) must agree bit-exactly on (action, counter
+slot), and the node path's hit counters must equal the per-table path's.
+"""
+import random
+
+import numpy as np
+import pytest
+
+import acl_fuzz as fz
+from oracle import gen
+from oracle.world import World
+from vpp_amd import _capi
+from vpp_amd import renderer as R
+from vpp_amd import workloads as W
+from vpp_amd._capi import MODE_CONN, MODE_PERPOD
+
+
+def topology(rnd, n_pods=14, weird=False, big=False):
+    """Local pods with random inbound/outbound ACLs on their TAPs (some reflective), two
+    remote pods, one pod without an interface, and ACLs on the node-output interface."""
+    e = R.Engine(0)
+    e.SetMainInterfaceName("GbE")
+    e.SetVxlanBVIIfName("VXLAN-BVI")
+    e.SetHostInterconnectIfName("VPP-Host")
+    local, ops, pod_ips, no_if = {}, [], [], []
+    for k in range(n_pods):
+        ip = 0x0A0A0000 | (k + 1)
+        pod_ips.append(ip)
+        another = k >= n_pods - 2
+        ifn = "tap%d" % k if not another and k != 3 else None
+        if ifn:
+            e.SetPodIfName("ns/p%d" % k, ifn)
+            local[ip] = ifn
+        e.RegisterPod("ns/p%d" % k, W.ip_str(ip), another)
+        if not ifn:
+            if not another:
+                no_if.append(ip)
+            continue
+        if rnd.random() < 0.6:
+            inb = ([{"action": 2, "src": "", "dst": ""}] if rnd.random() < 0.4 else
+                   fz.rand_acl(rnd, rnd.randint(0, 8), fz.ANCHORS + [ip], weird))
+            ops.append(("config/vpp/acls/v2/acl/in-" + ifn, {"name": "in-" + ifn, "rules": inb, "ingress": [ifn],
+                                                            "egress": []}))
+        if rnd.random() < 0.8:
+            outb = fz.rand_acl(rnd, rnd.randint(0, 40), fz.ANCHORS + pod_ips, weird, tail="deny")
+            ops.append(("config/vpp/acls/v2/acl/out-" + ifn, {"name": "out-" + ifn, "rules": outb, "ingress": [],
+                                                             "egress": [ifn]}))
+    glob = fz.rand_acl(rnd, 30, fz.ANCHORS + pod_ips, weird, tail="permit")
+    if big:  # one table past the cross-product limit (candidate mode): not covered by the node
+        glob = [{"action": k % 2, "src": "10.%d.%d.0/24" % (k // 256, k % 256), "dst": "",
+                 "udp": {"src": [0, 65535], "dst": [k % 1000, k % 1000 + 5]}} for k in range(17000)] + glob
+    ops.append(("config/vpp/acls/v2/acl/g", {"name": "g", "rules": glob, "ingress": [], "egress": ["VXLAN-BVI"]}))
+    e.ApplyTxn(True, ops)
+    return e, (local, no_if), pod_ips
+
+
+def tuples(seed, n, pod_ips, any_pct=0.02):
+    rng = np.random.default_rng(seed)
+    tup = list(fz.rand_tuples(rng, n, fz.ANCHORS + pod_ips, any_pct=any_pct))
+    for k in (0, 1):  # most end points are pods
+        m = rng.random(n) < 0.6
+        tup[k][m] = np.array(pod_ips, np.uint32)[rng.integers(0, len(pod_ips), int(m.sum()))]
+    return tuple(tup)
+
+
+def check(e, local, tup, expect_node=True):
+    src, dst, sport, dport, proto = tup
+    assert (e.node_stats() is not None) == expect_node
+    wd = World(e, local[0], "VXLAN-BVI", no_if_ips=local[1])
+    act, slot = wd.perpod(src, dst, dport, proto, threads=4)
+    pn, cpn = e.debug_classify_host(MODE_PERPOD, -1, *tup, counters=True, node=True)
+    pt, cpt = e.debug_classify_host(MODE_PERPOD, -1, *tup, counters=True, node=False)
+    assert np.array_equal(pn, pt)
+    assert np.array_equal(cpn, cpt)
+    assert np.array_equal(pn >> 30, act.astype(np.uint32)), np.nonzero((pn >> 30) != act)[0][:8]
+    assert np.array_equal(pn & 0x3FFFFFFF, slot)
+    assert np.array_equal(cpn, np.bincount(pn & 0x3FFFFFFF, minlength=len(cpn)))
+    conn, cslot = wd.conn(src, dst, sport, dport, proto, threads=4)
+    cn, ccn = e.debug_classify_host(MODE_CONN, -1, *tup, counters=True, node=True)
+    ct, cct = e.debug_classify_host(MODE_CONN, -1, *tup, counters=True, node=False)
+    assert np.array_equal(cn, ct)
+    assert np.array_equal(ccn, cct)
+    assert np.array_equal(cn >> 30, conn.astype(np.uint32)), np.nonzero((cn >> 30) != conn)[0][:8]
+    assert np.array_equal(cn & 0x3FFFFFFF, cslot)
+    return pn, cn
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_random_topologies(seed):
+    rnd = random.Random(2000 + seed)
+    e, local, pod_ips = topology(rnd, weird=seed % 2 == 1)
+    tup = tuples(seed, 20003 + seed, pod_ips)  # ragged: the kernels' one-tuple tail too
+    pn, cn = check(e, local, tup)
+    assert len(set((cn >> 30).tolist())) >= 2
+
+
+def test_table_over_cross_limit_falls_back_per_table():
+    rnd = random.Random(77)
+    e, local, pod_ips = topology(rnd, big=True)
+    assert e.table_stats(e.table_id("g"))["structure"] == "cand"
+    check(e, local, tuples(77, 8000, pod_ips))
+
+
+def test_node_disabled_and_rebuilt():
+    rnd = random.Random(5)
+    lib = _capi.lib
+    try:
+        assert lib.pg_set_tuning(b"node_build", 0) == 0
+        e, local, pod_ips = topology(rnd)
+        tup = tuples(5, 3000, pod_ips)
+        assert e.node_stats() is None
+        a = e.debug_classify_host(MODE_CONN, -1, *tup, node=True)  # falls back to per-table
+        check(e, local, tup, expect_node=False)
+    finally:
+        assert lib.pg_set_tuning(b"node_build", 1) == 0
+    e2, local2, _ = topology(random.Random(5))
+    assert e2.node_stats() is not None
+    assert np.array_equal(e2.debug_classify_host(MODE_CONN, -1, *tup, node=True), a)
+
+
+@pytest.mark.parametrize("root_bits", [4, 8, 16])
+def test_node_root_strides(root_bits):
+    lib = _capi.lib
+    try:
+        assert lib.pg_set_tuning(b"node_root_bits", root_bits) == 0
+        e, local, pod_ips = topology(random.Random(9))
+        check(e, local, tuples(9, 6000, pod_ips))
+    finally:
+        assert lib.pg_set_tuning(b"node_root_bits", 12) == 0
+
+
+def test_no_acls_and_unresolved_node_interface():
+    e = R.Engine(0)
+    e.SetMainInterfaceName("")  # no node-output interface: non-local addresses are unresolvable
+    e.SetPodIfName("ns/a", "tapA")
+    e.RegisterPod("ns/a", "10.0.0.1", False)
+    e.ApplyTxn(True, [("config/vpp/acls/v2/acl/x", {"name": "x", "rules": [{"action": 2, "src": "", "dst": ""}],
+                                                    "ingress": ["tapA"], "egress": []})])
+    tup = tuples(3, 2000, [0x0A000001])
+    pn = e.debug_classify_host(MODE_PERPOD, -1, *tup, node=True)
+    pt = e.debug_classify_host(MODE_PERPOD, -1, *tup, node=False)
+    assert np.array_equal(pn, pt)
+    cn = e.debug_classify_host(MODE_CONN, -1, *tup, node=True)
+    assert np.array_equal(cn, e.debug_classify_host(MODE_CONN, -1, *tup, node=False))
+    assert 3 in set((cn >> 30).tolist())  # FAILURE for unresolvable end points
+
+
+def test_config3_cluster_node_path():
+    """Config 3's topology (1k pods, ~9.6k rules): node size and host parity on a sample."""
+    w = W.config3(0, n_tuples=1 << 16)
+    e = w.engine
+    ns = e.node_stats()
+    assert ns is not None and ns["image_bytes"] <= 64 << 10, ns  # staged in LDS by the kernel
+    src, dst, sport, dport, proto = gen.gen_tuples(60001, **w.gen)
+    wd = World(e, w.local_ifs, w.node_if)
+    act, slot = wd.perpod(src, dst, dport, proto, threads=8)
+    got = e.debug_classify_host(MODE_PERPOD, -1, src, dst, sport, dport, proto, node=True)
+    assert np.array_equal(got >> 30, act.astype(np.uint32)) and np.array_equal(got & 0x3FFFFFFF, slot)
+    conn, cslot = wd.conn(src, dst, sport, dport, proto, threads=8)
+    got = e.debug_classify_host(MODE_CONN, -1, src, dst, sport, dport, proto, node=True)
+    assert np.array_equal(got >> 30, conn.astype(np.uint32)) and np.array_equal(got & 0x3FFFFFFF, cslot)

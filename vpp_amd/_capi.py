@@ -113,6 +113,10 @@ _SIGS = {
     "pg_table_stats": (C.c_int, [_P, C.c_int, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.POINTER(C.c_uint32),
                                  C.POINTER(C.c_uint32)]),
     "pg_debug_walk_blob": (C.c_int, [_P, C.c_char_p, _P, _P, _P, _P, C.c_uint64, _P]),
+    "pg_debug_classify_host": (C.c_int, [_P, C.c_int, C.c_int, C.POINTER(pg_tuple_soa), C.c_uint64, _P, _P,
+                                         C.c_int]),
+    "pg_node_stats": (C.c_int, [_P, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.POINTER(C.c_uint64),
+                                C.POINTER(C.c_uint64)]),
     "pg_classify_linear": (C.c_int, [_P, C.c_int, C.POINTER(pg_tuple_soa), C.c_uint64, _P, _P]),
     "pg_counters_device": (_P, [_P]),
     "pg_reset_counters": (C.c_int, [_P, _P]),

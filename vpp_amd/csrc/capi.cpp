@@ -5,7 +5,7 @@
 #include <stdexcept>
 
 #include "../../include/policygpu.h"
-#include "blobwalk.hpp"
+#include "classify.hpp"
 #include "engine.hpp"
 
 using namespace pg;
@@ -136,6 +136,18 @@ int pg_set_tuning(const char* key, int value) {
     if (std::string(key) == "root_bits_max") {  // applies to tables compiled afterwards
         if (value < 4 || value > 16) return PG_EINVAL;
         set_root_bits_max((uint32_t)value);
+        return PG_OK;
+    }
+    if (std::string(key) == "node_build" || std::string(key) == "node_root_bits") {  // tables compiled afterwards
+        static uint32_t enable = 1, bits = 12;
+        if (std::string(key) == "node_build") {
+            if (value != 0 && value != 1) return PG_EINVAL;
+            enable = (uint32_t)value;
+        } else {
+            if (value < 4 || value > 16) return PG_EINVAL;
+            bits = (uint32_t)value;
+        }
+        set_node_tuning(enable, bits);
         return PG_OK;
     }
     return dev_set_tuning(key, value) == 0 ? PG_OK : PG_EINVAL;
@@ -464,6 +476,98 @@ int pg_debug_walk_blob(pg_ctx* ctx, const char* acl_name, const uint32_t* src, c
             out[i0 + j] = w;
         }
     }
+    return PG_OK;
+    GUARD_END(ctx)
+}
+
+}  // extern "C"
+
+namespace {
+// host view of the compiled table set (pointers into the host image)
+DevTableSet host_view(const HostTableSet& h) {
+    DevTableSet v{};
+    v.rules = h.rules.data();
+    v.tabs = h.tabs.data();
+    v.blobs = h.blobs.data();
+    v.ifaces = h.ifaces.data();
+    v.iphash = h.iphash.data();
+    v.iphash_mask = h.iphash_mask;
+    v.node_if = h.node_if;
+    v.node_in = h.node_in;
+    v.node_out = h.node_out;
+    v.n_rules = (uint32_t)h.rules.size();
+    v.n_tables = (uint32_t)h.tabs.size();
+    v.n_ifaces = (uint32_t)(h.ifaces.size() / 2);
+    v.slot_noacl = v.n_rules + v.n_tables;
+    v.slot_unresolved = v.slot_noacl + 1;
+    v.n_slots = v.slot_unresolved + 1;
+    v.node = h.node;
+    v.node.img = h.node_img.empty() ? nullptr : h.node_img.data();
+    v.node.cross = h.node_img.empty() ? nullptr : h.node_cross.data();
+    return v;
+}
+
+template <int MODE, int Q>
+void host_q(const DevTableSet& T, bool node, int table_id, const pg_tuple_soa* t, uint64_t i, uint32_t* out,
+            const Hist& h) {
+    uint32_t s[Q], d[Q], sp[Q], dp[Q], pr[Q], o[Q];
+    for (int j = 0; j < Q; j++) {
+        s[j] = t->src_ip[i + j], d[j] = t->dst_ip[i + j], dp[j] = t->dst_port[i + j], pr[j] = t->proto[i + j];
+        sp[j] = MODE == 2 ? t->src_port[i + j] : 0u;
+    }
+    if constexpr (MODE == 0) {
+        classify_q<0, true, Q>(T, T.blobs, load_tab(T.tabs, table_id), s, d, sp, dp, pr, h, o);
+    } else {
+        if (node) classify_node_q<MODE, true, Q>(T, T.node, DevLoader{T.node.img}, s, d, sp, dp, pr, h, o);
+        else classify_q<MODE, true, Q>(T, T.blobs, DevTable{}, s, d, sp, dp, pr, h, o);
+    }
+    for (int j = 0; j < Q; j++) out[i + j] = o[j];
+}
+
+template <int MODE>
+void host_classify(const DevTableSet& T, bool node, int table_id, const pg_tuple_soa* t, uint64_t n, uint32_t* out,
+                   const Hist& h) {
+    const uint64_t nq = n & ~(uint64_t)3;  // the kernels' quads, then one tuple at a time
+    for (uint64_t i = 0; i < nq; i += 4) host_q<MODE, 4>(T, node, table_id, t, i, out, h);
+    for (uint64_t i = nq; i < n; i++) host_q<MODE, 1>(T, node, table_id, t, i, out, h);
+}
+}  // namespace
+
+extern "C" {
+
+int pg_debug_classify_host(pg_ctx* ctx, int mode, int table_id, const pg_tuple_soa* t, uint64_t n, uint32_t* out,
+                           uint64_t* counters, int node) {
+    if (!ctx || !t || mode < 0 || mode > 2) return PG_EINVAL;
+    GUARD_BEGIN
+    Engine& E = ctx->eng;
+    if (!E.compiled) E.compile();
+    const DevTableSet T = host_view(E.host);
+    if (mode == PG_MODE_SINGLE && (table_id < 0 || (uint32_t)table_id >= T.n_tables))
+        return fail(ctx, PG_EINVAL, "table id out of range");
+    if (n == 0) return PG_OK;
+    if (!out || !t->src_ip || !t->dst_ip || !t->dst_port || !t->proto || (mode == PG_MODE_CONN && !t->src_port))
+        return fail(ctx, PG_EINVAL, "missing tuple field");
+    const bool use_node = node && T.node.img != nullptr;
+    const Hist h{nullptr, (unsigned long long*)counters};
+    if (mode == 0) host_classify<0>(T, false, table_id, t, n, out, h);
+    else if (mode == 1) host_classify<1>(T, use_node, table_id, t, n, out, h);
+    else host_classify<2>(T, use_node, table_id, t, n, out, h);
+    return PG_OK;
+    GUARD_END(ctx)
+}
+
+int pg_node_stats(pg_ctx* ctx, uint32_t* ip_classes, uint32_t* key_classes, uint64_t* image_bytes,
+                  uint64_t* cross_bytes) {
+    if (!ctx) return PG_EINVAL;
+    GUARD_BEGIN
+    Engine& E = ctx->eng;
+    if (!E.compiled) E.compile();
+    const HostTableSet& h = E.host;
+    if (h.node_img.empty()) return fail(ctx, PG_ENOENT, "no node classifier (disabled or over budget)");
+    if (ip_classes) *ip_classes = h.node.n_ipc;
+    if (key_classes) *key_classes = h.node.gk;
+    if (image_bytes) *image_bytes = h.node_img.size() * 4;
+    if (cross_bytes) *cross_bytes = h.node_cross.size() * 4;
     return PG_OK;
     GUARD_END(ctx)
 }

@@ -1,0 +1,505 @@
+// Per-tuple semantics of the classify path, written once for both sides: the gfx950 kernels
+// (device.hip) instantiate it with LDS / global loaders, and pg_debug_classify_host (tests
+// only, never on the classify path) instantiates it on the host, so every compiled structure
+// -- per-table blobs, the node classifier, interface resolution, the testConnection fusion --
+// is checked against the oracle on CPU with the code the GPU runs.
+//
+// One evaluation == evalACL (mock/aclengine/aclengine_mock.go:503-652) over the ACL a table
+// was compiled from (engine.cpp compile_acl_rule); the output word packs the ACLAction (or
+// ConnAction) in bits 31-30 and the deciding counter slot in bits 29-0.
+//
+// Every function works on Q tuples of one lane "in lockstep": each dependent step issues the
+// loads of all Q tuples before consuming any, so a lane has up to Q independent chains in
+// flight (Q = 4 in the kernels' main loop, 1 in the remainder loop).
+#pragma once
+#include <cstdint>
+
+#include "blobwalk.hpp"
+#include "device.hpp"
+
+namespace pg {
+
+#if defined(__HIP_DEVICE_COMPILE__)
+#define PG_NOINLINE __device__ __noinline__
+#else
+#define PG_NOINLINE inline
+#endif
+
+PG_HD uint32_t pkt_key(uint32_t proto, uint32_t port) {
+    return proto == 0u ? port : (proto == 1u ? (kKeyUDP | port) : (proto == 2u ? kKeyOTHER : kKeyANY));
+}
+PG_HD uint32_t verdict(uint32_t act, uint32_t slot) { return (act << 30) | slot; }
+constexpr uint32_t kSlotMask = 0x3FFFFFFFu;
+
+PG_HD uint32_t hash_ip(uint32_t ip) {
+    ip ^= ip >> 16;
+    ip *= 0x7feb352du;
+    ip ^= ip >> 15;
+    ip *= 0x846ca68bu;
+    ip ^= ip >> 16;
+    return ip;
+}
+
+// Linear first-match over a table's compiled rules: LINEAR tables and ANY-protocol packets
+// (rare). Scalar arguments only, so the call needs no stack frame.
+PG_NOINLINE uint32_t eval_linear(const DevRule* rules, uint32_t base, uint32_t nr, uint32_t dflt, uint32_t src,
+                                 uint32_t dst, uint32_t key) {
+    const bool any = key >= kKeyANY;
+    for (uint32_t i = 0; i < nr; i++) {
+        const DevRule r = rules[base + i];
+        if ((src & r.smask) != r.snet || (dst & r.dmask) != r.dnet) continue;
+        if (any) {
+            if ((r.act >> 4) != kActNever) return verdict((r.act >> 4) & 3u, base + i);
+        } else if (key >= r.klo && key <= r.khi) {
+            return verdict(r.act & 3u, base + i);
+        }
+    }
+    return dflt;
+}
+
+// 16/8/4-byte loads from LDS or global memory (the device infers the address space).
+struct DevLoader {
+    const uint32_t* b;
+    PG_HD uint32_t u32(uint32_t i) const { return b[i]; }
+    PG_HD W2 u2(uint32_t i) const {
+#if defined(__HIP_DEVICE_COMPILE__)
+        const uint2 v = *reinterpret_cast<const uint2*>(b + i);
+        return W2{v.x, v.y};
+#else
+        return W2{b[i], b[i + 1]};
+#endif
+    }
+    PG_HD W4 u4(uint32_t i) const {
+#if defined(__HIP_DEVICE_COMPILE__)
+        const uint4 v = *reinterpret_cast<const uint4*>(b + i);
+        return W4{v.x, v.y, v.z, v.w};
+#else
+        return W4{b[i], b[i + 1], b[i + 2], b[i + 3]};
+#endif
+    }
+};
+
+PG_HD DevTable load_tab(const DevTable* tabs, int32_t t) {
+    const DevLoader l{reinterpret_cast<const uint32_t*>(tabs + t)};
+    const W4 a = l.u4(0), c = l.u4(4);
+    return DevTable{a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w};
+}
+
+// evalACL of Q tuples against their tables' per-table blobs, in lockstep.
+// act[j]: evaluate tuple j against tab[j]; blobs: base the tables' blob_off is relative to
+// (the global blob array, or the LDS copy of a staged table).
+template <int Q>
+PG_HD void eval_q(const DevTableSet& T, const uint32_t* blobs, const DevTable (&tab)[Q], const bool (&act)[Q],
+                  const uint32_t (&src)[Q], const uint32_t (&dst)[Q], const uint32_t (&key)[Q], uint32_t (&w)[Q]) {
+    DevLoader ld[Q];
+    BlobTab tb[Q];
+    bool on[Q];
+    PG_UNROLL
+    for (int j = 0; j < Q; j++) {
+        ld[j] = DevLoader{blobs + tab[j].blob_off};
+        tb[j] = BlobTab{tab[j].fsk, tab[j].dflt, tab[j].kroot, tab[j].xoff, tab[j].nkc};
+        on[j] = act[j] && !(tab[j].fsk & kFlagLinear) && key[j] < kWalkKeyLimit;
+    }
+    blob_walk(ld, tb, on, src, dst, key, w);
+    PG_UNROLL
+    for (int j = 0; j < Q; j++)
+        if (act[j] && !on[j])
+            w[j] = eval_linear(T.rules, tab[j].rule_base, tab[j].n_rules, tab[j].dflt, src[j], dst[j], key[j]);
+}
+
+// tables of a connection end point: interface (-1/-2 unresolvable) and its ACLs
+struct End {
+    int32_t ifc, tin, tout;
+};
+
+// IPv4 -> end point by the iphash (per-table path): a local pod's TAP, else the node-output
+// interface (VXLAN BVI or main; aclengine_mock.go:273-420). One 16-B load per probe step.
+template <int Q>
+PG_HD void probe_q(const DevTableSet& T, const uint32_t (&ip)[Q], End (&e)[Q]) {
+    const DevLoader H{T.iphash};
+    uint32_t s[Q];
+    W4 v[Q];
+    bool pend[Q];
+    PG_UNROLL
+    for (int j = 0; j < Q; j++) {
+        s[j] = hash_ip(ip[j]) & T.iphash_mask;
+        v[j] = H.u4(4u * s[j]);
+        pend[j] = true;
+    }
+    for (;;) {
+        bool more = false;
+        PG_UNROLL
+        for (int j = 0; j < Q; j++) {
+            if (!pend[j]) continue;
+            if (v[j].y == 0xFFFFFFFFu) {
+                e[j] = End{T.node_if, T.node_in, T.node_out};
+                pend[j] = false;
+            } else if (v[j].x == ip[j]) {
+                e[j] = End{(int32_t)v[j].y, (int32_t)v[j].z, (int32_t)v[j].w};
+                pend[j] = false;
+            } else {
+                s[j] = (s[j] + 1u) & T.iphash_mask;
+                v[j] = H.u4(4u * s[j]);
+                more = true;
+            }
+        }
+        if (!more) break;
+    }
+}
+
+// per-rule hit counters: LDS histogram (u32) or global u64 slots on the device, plain u64
+// slots on the host
+struct Hist {
+    uint32_t* lds;
+    unsigned long long* glob;
+    PG_HD void inc(uint32_t slot) const {
+#if defined(__HIP_DEVICE_COMPILE__)
+        if (lds) atomicAdd(&lds[slot], 1u);
+        else if (glob) atomicAdd(&glob[slot], 1ull);
+#else
+        if (glob) glob[slot]++;
+#endif
+    }
+};
+
+// ---- evaluators: evalACL of Q tuples on tables t[j], forward (src -> dst, SYN key) or
+// reverse (dst -> src, SYN-ACK key; testConnection's second half) ----------------------------
+
+// per-table blobs (global memory)
+template <int Q>
+struct TabEval {
+    const DevTableSet& T;
+    const uint32_t (&src)[Q];
+    const uint32_t (&dst)[Q];
+    const uint32_t (&ksyn)[Q];
+    const uint32_t (&kack)[Q];
+    PG_HD void operator()(const int32_t (&t)[Q], const bool (&act)[Q], bool rev, uint32_t (&w)[Q]) const {
+        DevTable tab[Q];
+        PG_UNROLL
+        for (int j = 0; j < Q; j++) tab[j] = act[j] ? load_tab(T.tabs, t[j]) : DevTable{};
+        eval_q(T, T.blobs, tab, act, rev ? dst : src, rev ? src : dst, rev ? kack : ksyn, w);
+    }
+};
+
+// Node classifier (fastpath.cpp build_node): IPv4 -> node IP class and L4 key -> node key
+// class by tries in the node image (LDS when staged), then one entry of the node cross
+// table per evaluation, cross[tabinfo[t].base + ipclass * nkc_t + kmap[t][keyclass]]: a
+// verdict, or (kNodeList) the first of the dst records to test. Tables the node does not
+// cover, LINEAR tables and ANY-protocol packets take the per-table path.
+// Q trie lookups in lockstep (root stride s1 over a W-bit address, then 8-bit strides)
+template <class L, int Q>
+PG_HD void node_trie_q(const L& ld, uint32_t root, uint32_t s1, uint32_t W, const uint32_t (&a)[Q], uint32_t (&c)[Q]) {
+    uint32_t sh[Q], e[Q];
+    PG_UNROLL
+    for (int j = 0; j < Q; j++) {
+        sh[j] = W - s1;
+        e[j] = ld.u32(root + (a[j] >> sh[j]));
+    }
+    for (;;) {
+        bool more = false;
+        PG_UNROLL
+        for (int j = 0; j < Q; j++) more |= !(e[j] & kLeaf);
+        if (!more) break;
+        PG_UNROLL
+        for (int j = 0; j < Q; j++) {
+            if (e[j] & kLeaf) continue;
+            const uint32_t st = sh[j] < 8u ? sh[j] : 8u;
+            sh[j] -= st;
+            e[j] = ld.u32(e[j] + ((a[j] >> sh[j]) & ((1u << st) - 1u)));
+        }
+    }
+    PG_UNROLL
+    for (int j = 0; j < Q; j++) c[j] = e[j] & ~kLeaf;
+}
+
+// end point of a node IP class (ipinfo: {interface, tin | tout << 16}, 0xFFFF = no ACL)
+template <class L>
+PG_HD End node_end(const L& img, const DevNode& N, uint32_t ipc) {
+    const W2 v = img.u2(N.ipinfo + 2u * ipc);
+    const uint32_t tin = v.y & 0xFFFFu, tout = v.y >> 16;
+    return End{(int32_t)v.x, tin == 0xFFFFu ? -1 : (int32_t)tin, tout == 0xFFFFu ? -1 : (int32_t)tout};
+}
+
+template <class L, int Q>
+struct NodeEval {
+    const DevTableSet& T;
+    const DevNode& N;
+    const L& img;
+    const uint32_t (&src)[Q];
+    const uint32_t (&dst)[Q];
+    const uint32_t (&ksyn)[Q];
+    const uint32_t (&kack)[Q];
+    const uint32_t (&cs)[Q];  // node IP class of src
+    const uint32_t (&cd)[Q];  // node IP class of dst
+    const uint32_t (&gsyn)[Q];  // node key class of the SYN key
+    const uint32_t (&gack)[Q];
+    PG_HD void operator()(const int32_t (&t)[Q], const bool (&act)[Q], bool rev, uint32_t (&w)[Q]) const {
+        const DevLoader X{N.cross};
+        const uint32_t(&a)[Q] = rev ? dst : src;
+        const uint32_t(&b)[Q] = rev ? src : dst;
+        const uint32_t(&k)[Q] = rev ? kack : ksyn;
+        const uint32_t(&ca)[Q] = rev ? cd : cs;
+        const uint32_t(&gk)[Q] = rev ? gack : gsyn;
+        bool on[Q], fb[Q], pend[Q];
+        uint32_t pos[Q];
+        PG_UNROLL
+        for (int j = 0; j < Q; j++) {
+            on[j] = false;
+            if (act[j] && k[j] < kWalkKeyLimit) {
+                const W2 ti = img.u2(N.tabinfo + 2u * (uint32_t)t[j]);  // {cross base, nkc | covered << 31}
+                if (ti.y >> 31) {
+                    const uint32_t ki = (uint32_t)t[j] * N.gk + gk[j];
+                    const uint32_t lk = (img.u32(N.kmap + (ki >> 1)) >> ((ki & 1u) * 16u)) & 0xFFFFu;
+                    pos[j] = ti.x + ca[j] * (ti.y & 0xFFFFu) + lk;
+                    on[j] = true;
+                }
+            }
+            fb[j] = act[j] && !on[j];
+        }
+        PG_UNROLL
+        for (int j = 0; j < Q; j++) {
+            pend[j] = false;
+            if (!on[j]) continue;
+            const uint32_t e = X.u32(pos[j]);
+            w[j] = e;
+            pend[j] = (e & kNodeList) != 0u;
+            pos[j] = (e & kNodeRecMask) << 2;
+        }
+        // dst records until the first match (every list ends with a match-all record)
+        for (;;) {
+            bool more = false;
+            PG_UNROLL
+            for (int j = 0; j < Q; j++) more |= pend[j];
+            if (!more) break;
+            PG_UNROLL
+            for (int j = 0; j < Q; j++) {
+                if (!pend[j]) continue;
+                const W4 r = X.u4(pos[j]);
+                if (rec_match(r, b[j], k[j])) {
+                    w[j] = r.w;
+                    pend[j] = false;
+                } else {
+                    pos[j] += 4u;
+                }
+            }
+        }
+        bool anyfb = false;
+        PG_UNROLL
+        for (int j = 0; j < Q; j++) anyfb |= fb[j];
+        if (anyfb) {
+            DevTable tab[Q];
+            PG_UNROLL
+            for (int j = 0; j < Q; j++) tab[j] = fb[j] ? load_tab(T.tabs, t[j]) : DevTable{};
+            uint32_t wf[Q];
+            eval_q(T, T.blobs, tab, fb, a, b, k, wf);
+            PG_UNROLL
+            for (int j = 0; j < Q; j++)
+                if (fb[j]) w[j] = wf[j];
+        }
+    }
+};
+
+// one evalACL step of testConnection / per-pod mode: tables t[j] (-1 = no ACL: PERMIT)
+template <int Q, bool COUNT, class EV>
+PG_HD void eval_step(const DevTableSet& T, const EV& ev, const int32_t (&t)[Q], const bool (&run)[Q], bool rev,
+                     const Hist& h, uint32_t (&w)[Q]) {
+    bool act[Q];
+    PG_UNROLL
+    for (int j = 0; j < Q; j++) {
+        act[j] = run[j] && t[j] >= 0;
+        if (run[j] && t[j] < 0) w[j] = verdict(kActPermit, T.slot_noacl);  // nil ACL (:506-508)
+    }
+    ev(t, act, rev, w);
+    if (COUNT) {
+        PG_UNROLL
+        for (int j = 0; j < Q; j++)
+            if (run[j]) h.inc(w[j] & kSlotMask);
+    }
+}
+
+// testConnection (aclengine_mock.go:424-501) of Q connections on resolved end points, each
+// of its up-to-4 evalACL steps in lockstep over the Q connections.
+template <int Q, bool COUNT, class EV>
+PG_HD void conn_q(const DevTableSet& T, const EV& ev, const End (&es)[Q], const End (&ed)[Q], const Hist& h,
+                  uint32_t (&out)[Q]) {
+    bool live[Q], srefl[Q], drefl[Q], same[Q], run[Q];
+    uint32_t w[Q];
+    int32_t t[Q];
+    PG_UNROLL
+    for (int j = 0; j < Q; j++) {
+        live[j] = es[j].ifc >= 0 && ed[j].ifc >= 0;
+        srefl[j] = drefl[j] = false;
+        same[j] = es[j].ifc == ed[j].ifc;
+        w[j] = 0;
+        if (!live[j]) {
+            out[j] = verdict(3u, T.slot_unresolved);
+            if (COUNT) h.inc(T.slot_unresolved);
+        }
+    }
+    // SYN: src interface inbound
+    PG_UNROLL
+    for (int j = 0; j < Q; j++) t[j] = es[j].tin, run[j] = live[j];
+    eval_step<Q, COUNT>(T, ev, t, run, false, h, w);
+    PG_UNROLL
+    for (int j = 0; j < Q; j++) {
+        if (!run[j]) continue;
+        const uint32_t a = w[j] >> 30;
+        if (a == kActFailure || a == kActDeny) {
+            out[j] = verdict(a == kActFailure ? 3u : 0u, w[j] & kSlotMask);
+            live[j] = false;
+        } else if (a == kActReflect) {
+            srefl[j] = true;
+            drefl[j] = same[j];
+        }
+    }
+    // SYN: dst interface outbound
+    PG_UNROLL
+    for (int j = 0; j < Q; j++) t[j] = ed[j].tout, run[j] = live[j] && !drefl[j];
+    eval_step<Q, COUNT>(T, ev, t, run, false, h, w);
+    PG_UNROLL
+    for (int j = 0; j < Q; j++) {
+        if (!run[j]) continue;
+        const uint32_t a = w[j] >> 30;
+        if (a == kActFailure || a == kActDeny) {
+            out[j] = verdict(a == kActFailure ? 3u : 0u, w[j] & kSlotMask);
+            live[j] = false;
+        } else if (a == kActReflect) {
+            drefl[j] = true;
+            if (same[j]) srefl[j] = true;
+        }
+    }
+    // SYN-ACK: dst interface inbound
+    PG_UNROLL
+    for (int j = 0; j < Q; j++) t[j] = ed[j].tin, run[j] = live[j] && !drefl[j];
+    eval_step<Q, COUNT>(T, ev, t, run, true, h, w);
+    PG_UNROLL
+    for (int j = 0; j < Q; j++) {
+        if (!run[j]) continue;
+        const uint32_t a = w[j] >> 30;
+        if (a == kActFailure || a == kActDeny) {
+            out[j] = verdict(a == kActFailure ? 3u : 1u, w[j] & kSlotMask);
+            live[j] = false;
+        }
+    }
+    // SYN-ACK: src interface outbound
+    PG_UNROLL
+    for (int j = 0; j < Q; j++) t[j] = es[j].tout, run[j] = live[j] && !srefl[j];
+    eval_step<Q, COUNT>(T, ev, t, run, true, h, w);
+    PG_UNROLL
+    for (int j = 0; j < Q; j++) {
+        if (!live[j]) continue;
+        const uint32_t a = w[j] >> 30;
+        if (run[j] && (a == kActFailure || a == kActDeny)) out[j] = verdict(a == kActFailure ? 3u : 1u, w[j] & kSlotMask);
+        else out[j] = verdict(2u, w[j] & kSlotMask);  // allowed; slot of the last evaluation
+    }
+}
+
+// Q tuples of one lane, any mode, per-table path. SINGLE: tab0 is the (uniform) table, its
+// blob at `blobs`.
+template <int MODE, bool COUNT, int Q>
+PG_HD void classify_q(const DevTableSet& T, const uint32_t* blobs, const DevTable& tab0, const uint32_t (&s)[Q],
+                      const uint32_t (&d)[Q], const uint32_t (&sp)[Q], const uint32_t (&dp)[Q],
+                      const uint32_t (&pr)[Q], const Hist& h, uint32_t (&out)[Q]) {
+    uint32_t key[Q], kack[Q];
+    PG_UNROLL
+    for (int j = 0; j < Q; j++) key[j] = pkt_key(pr[j], dp[j]), kack[j] = pkt_key(pr[j], sp[j]);
+    if (MODE == 0) {  // SINGLE
+        DevTable tab[Q];
+        bool act[Q];
+        PG_UNROLL
+        for (int j = 0; j < Q; j++) tab[j] = tab0, act[j] = true;
+        eval_q(T, blobs, tab, act, s, d, key, out);
+        if (COUNT) {
+            PG_UNROLL
+            for (int j = 0; j < Q; j++) h.inc(out[j] & kSlotMask);
+        }
+        return;
+    }
+    const TabEval<Q> ev{T, s, d, key, kack};
+    if (MODE == 1) {  // PERPOD: outbound ACL of the interface dst is reached by
+        End e[Q];
+        probe_q(T, d, e);
+        int32_t t[Q];
+        bool run[Q];
+        PG_UNROLL
+        for (int j = 0; j < Q; j++) {
+            run[j] = e[j].ifc >= 0;
+            t[j] = e[j].tout;
+            if (!run[j]) {
+                out[j] = verdict(kActFailure, T.slot_unresolved);
+                if (COUNT) h.inc(T.slot_unresolved);
+            }
+        }
+        eval_step<Q, COUNT>(T, ev, t, run, false, h, out);
+    } else {  // CONN
+        uint32_t ips[2 * Q];
+        End e[2 * Q];
+        PG_UNROLL
+        for (int j = 0; j < Q; j++) ips[j] = s[j], ips[Q + j] = d[j];
+        probe_q(T, ips, e);
+        End es[Q], ed[Q];
+        PG_UNROLL
+        for (int j = 0; j < Q; j++) es[j] = e[j], ed[j] = e[Q + j];
+        conn_q<Q, COUNT>(T, ev, es, ed, h, out);
+    }
+}
+
+// Q tuples of one lane, PERPOD / CONN, node path. `img` reads the node image (LDS copy or
+// global memory).
+template <int MODE, bool COUNT, int Q, class L>
+PG_HD void classify_node_q(const DevTableSet& T, const DevNode& N, const L& img, const uint32_t (&s)[Q],
+                           const uint32_t (&d)[Q], const uint32_t (&sp)[Q], const uint32_t (&dp)[Q],
+                           const uint32_t (&pr)[Q], const Hist& h, uint32_t (&out)[Q]) {
+    uint32_t key[Q], kack[Q];
+    PG_UNROLL
+    for (int j = 0; j < Q; j++) key[j] = pkt_key(pr[j], dp[j]), kack[j] = MODE == 2 ? pkt_key(pr[j], sp[j]) : key[j];
+    // node IP classes of src and dst, node key classes of both keys: 2Q + 2Q trie walks
+    uint32_t ips[2 * Q], ipc[2 * Q];
+    PG_UNROLL
+    for (int j = 0; j < Q; j++) ips[j] = s[j], ips[Q + j] = d[j];
+    node_trie_q(img, 0u, N.ip_s1, 32u, ips, ipc);
+    uint32_t cs[Q], cd[Q], gs[Q], ga[Q];
+    if (MODE == 2) {
+        uint32_t keys[2 * Q], kc[2 * Q];
+        PG_UNROLL
+        for (int j = 0; j < Q; j++) {
+            keys[j] = key[j] < kWalkKeyLimit ? key[j] : 0u;
+            keys[Q + j] = kack[j] < kWalkKeyLimit ? kack[j] : 0u;
+        }
+        node_trie_q(img, N.key_root, N.key_k1, 18u, keys, kc);
+        PG_UNROLL
+        for (int j = 0; j < Q; j++) gs[j] = kc[j], ga[j] = kc[Q + j];
+    } else {
+        uint32_t keys[Q];
+        PG_UNROLL
+        for (int j = 0; j < Q; j++) keys[j] = key[j] < kWalkKeyLimit ? key[j] : 0u;
+        node_trie_q(img, N.key_root, N.key_k1, 18u, keys, gs);
+        PG_UNROLL
+        for (int j = 0; j < Q; j++) ga[j] = gs[j];
+    }
+    PG_UNROLL
+    for (int j = 0; j < Q; j++) cs[j] = ipc[j], cd[j] = ipc[Q + j];
+    const NodeEval<L, Q> ev{T, N, img, s, d, key, kack, cs, cd, gs, ga};
+    if (MODE == 1) {
+        int32_t t[Q];
+        bool run[Q];
+        PG_UNROLL
+        for (int j = 0; j < Q; j++) {
+            const End e = node_end(img, N, cd[j]);
+            run[j] = e.ifc >= 0;
+            t[j] = e.tout;
+            if (!run[j]) {
+                out[j] = verdict(kActFailure, T.slot_unresolved);
+                if (COUNT) h.inc(T.slot_unresolved);
+            }
+        }
+        eval_step<Q, COUNT>(T, ev, t, run, false, h, out);
+    } else {
+        End es[Q], ed[Q];
+        PG_UNROLL
+        for (int j = 0; j < Q; j++) es[j] = node_end(img, N, cs[j]), ed[j] = node_end(img, N, cd[j]);
+        conn_q<Q, COUNT>(T, ev, es, ed, h, out);
+    }
+}
+
+}  // namespace pg

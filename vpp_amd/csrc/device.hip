@@ -22,8 +22,7 @@
 #include <algorithm>
 #include <cstring>
 
-#include "blobwalk.hpp"
-#include "device.hpp"
+#include "classify.hpp"
 
 namespace pg {
 
@@ -92,6 +91,8 @@ DeviceBuffers* dev_upload(const HostTableSet& h, std::string* err) {
     size_t o_blob = place(h.blobs.size() * 4);
     size_t o_if = place(h.ifaces.size() * 4);
     size_t o_ip = place(h.iphash.size() * 4);
+    size_t o_nimg = place(h.node_img.size() * 4);
+    size_t o_nx = place(h.node_cross.size() * 4);
     std::vector<uint8_t> img(off, 0);
     auto put = [&](size_t o, const void* p, size_t n) {
         if (n) std::memcpy(img.data() + o, p, n);
@@ -101,6 +102,8 @@ DeviceBuffers* dev_upload(const HostTableSet& h, std::string* err) {
     put(o_blob, h.blobs.data(), h.blobs.size() * 4);
     put(o_if, h.ifaces.data(), h.ifaces.size() * 4);
     put(o_ip, h.iphash.data(), h.iphash.size() * 4);
+    put(o_nimg, h.node_img.data(), h.node_img.size() * 4);
+    put(o_nx, h.node_cross.data(), h.node_cross.size() * 4);
     auto* b = new DeviceBuffers();
     b->blob = dev_alloc(off, err);
     if (!b->blob) {
@@ -129,6 +132,9 @@ DeviceBuffers* dev_upload(const HostTableSet& h, std::string* err) {
     v.slot_noacl = v.n_rules + v.n_tables;
     v.slot_unresolved = v.slot_noacl + 1;
     v.n_slots = v.slot_unresolved + 1;
+    v.node = h.node;
+    v.node.img = h.node_img.empty() ? nullptr : (const uint32_t*)(base + o_nimg);
+    v.node.cross = h.node_img.empty() ? nullptr : (const uint32_t*)(base + o_nx);
     b->host_tabs = h.tabs;
     b->host_blob_words = h.blob_words;
     v.host_tabs = b->host_tabs.data();
@@ -141,278 +147,6 @@ void dev_free(DeviceBuffers* b) {
     (void)hipDeviceSynchronize();
     dev_release(b->blob);
     delete b;
-}
-
-// ---------------------------------------------------------------------------------------------
-// device helpers
-// ---------------------------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t pkt_key(uint32_t proto, uint32_t port) {
-    return proto == 0u ? port : (proto == 1u ? (kKeyUDP | port) : (proto == 2u ? kKeyOTHER : kKeyANY));
-}
-__device__ __forceinline__ uint32_t verdict(uint32_t act, uint32_t slot) { return (act << 30) | slot; }
-constexpr uint32_t kSlotMask = 0x3FFFFFFFu;
-
-// Linear first-match over a table's compiled rules: LINEAR tables and ANY-protocol packets
-// (rare). Scalar arguments only, so the call needs no stack frame.
-__device__ __noinline__ uint32_t eval_linear(const DevRule* rules, uint32_t base, uint32_t nr, uint32_t dflt,
-                                             uint32_t src, uint32_t dst, uint32_t key) {
-    const bool any = key >= kKeyANY;
-    for (uint32_t i = 0; i < nr; i++) {
-        const DevRule r = rules[base + i];
-        if ((src & r.smask) != r.snet || (dst & r.dmask) != r.dnet) continue;
-        if (any) {
-            if ((r.act >> 4) != kActNever) return verdict((r.act >> 4) & 3u, base + i);
-        } else if (key >= r.klo && key <= r.khi) {
-            return verdict(r.act & 3u, base + i);
-        }
-    }
-    return dflt;
-}
-
-struct DevLoader {  // 16/8/4-byte loads from LDS or global memory (address space inferred)
-    const uint32_t* b;
-    __device__ __forceinline__ uint32_t u32(uint32_t i) const { return b[i]; }
-    __device__ __forceinline__ W2 u2(uint32_t i) const {
-        const uint2 v = *reinterpret_cast<const uint2*>(b + i);
-        return W2{v.x, v.y};
-    }
-    __device__ __forceinline__ W4 u4(uint32_t i) const {
-        const uint4 v = *reinterpret_cast<const uint4*>(b + i);
-        return W4{v.x, v.y, v.z, v.w};
-    }
-};
-
-__device__ __forceinline__ DevTable load_tab(const DevTable* tabs, int32_t t) {
-    const uint4* p = reinterpret_cast<const uint4*>(tabs + t);
-    const uint4 a = p[0], c = p[1];
-    return DevTable{a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w};
-}
-
-// evalACL (aclengine_mock.go:503-652) of Q tuples against their tables, in lockstep.
-// act[j]: evaluate tuple j against tab[j]; blobs: base the tables' blob_off is relative to
-// (the global blob array, or the LDS copy of a staged table).
-template <int Q>
-__device__ __forceinline__ void eval_q(const DevTableSet& T, const uint32_t* blobs, const DevTable (&tab)[Q],
-                                       const bool (&act)[Q], const uint32_t (&src)[Q], const uint32_t (&dst)[Q],
-                                       const uint32_t (&key)[Q], uint32_t (&w)[Q]) {
-    DevLoader ld[Q];
-    BlobTab tb[Q];
-    bool on[Q];
-#pragma unroll
-    for (int j = 0; j < Q; j++) {
-        ld[j] = DevLoader{blobs + tab[j].blob_off};
-        tb[j] = BlobTab{tab[j].fsk, tab[j].dflt, tab[j].kroot, tab[j].xoff, tab[j].nkc};
-        on[j] = act[j] && !(tab[j].fsk & kFlagLinear) && key[j] < kWalkKeyLimit;
-    }
-    blob_walk(ld, tb, on, src, dst, key, w);
-#pragma unroll
-    for (int j = 0; j < Q; j++)
-        if (act[j] && !on[j])
-            w[j] = eval_linear(T.rules, tab[j].rule_base, tab[j].n_rules, tab[j].dflt, src[j], dst[j], key[j]);
-}
-
-// tables of a connection end point: interface (-1/-2 unresolvable) and its ACLs
-struct End {
-    int32_t ifc, tin, tout;
-};
-
-__device__ __forceinline__ uint32_t hash_ip(uint32_t ip) {
-    ip ^= ip >> 16;
-    ip *= 0x7feb352du;
-    ip ^= ip >> 15;
-    ip *= 0x846ca68bu;
-    ip ^= ip >> 16;
-    return ip;
-}
-// IPv4 -> end point: a local pod's TAP, else the node-output interface (VXLAN BVI or main;
-// aclengine_mock.go:273-420). Q probes in lockstep, one 16-B load per probe step.
-template <int Q>
-__device__ __forceinline__ void probe_q(const DevTableSet& T, const uint32_t (&ip)[Q], End (&e)[Q]) {
-    const uint4* H = reinterpret_cast<const uint4*>(T.iphash);
-    uint32_t s[Q];
-    uint4 v[Q];
-    bool pend[Q];
-#pragma unroll
-    for (int j = 0; j < Q; j++) {
-        s[j] = hash_ip(ip[j]) & T.iphash_mask;
-        v[j] = H[s[j]];
-        pend[j] = true;
-    }
-    for (;;) {
-        bool more = false;
-#pragma unroll
-        for (int j = 0; j < Q; j++) {
-            if (!pend[j]) continue;
-            if (v[j].y == 0xFFFFFFFFu) {
-                e[j] = End{T.node_if, T.node_in, T.node_out};
-                pend[j] = false;
-            } else if (v[j].x == ip[j]) {
-                e[j] = End{(int32_t)v[j].y, (int32_t)v[j].z, (int32_t)v[j].w};
-                pend[j] = false;
-            } else {
-                s[j] = (s[j] + 1u) & T.iphash_mask;
-                v[j] = H[s[j]];
-                more = true;
-            }
-        }
-        if (!more) break;
-    }
-}
-
-struct Hist {
-    uint32_t* lds;
-    unsigned long long* glob;
-    __device__ __forceinline__ void inc(uint32_t slot) const {
-        if (lds) atomicAdd(&lds[slot], 1u);
-        else if (glob) atomicAdd(&glob[slot], 1ull);
-    }
-};
-
-// one evalACL step of testConnection / per-pod mode: tables t[j] (-1 = no ACL: PERMIT)
-template <int Q, bool COUNT>
-__device__ __forceinline__ void eval_step(const DevTableSet& T, const int32_t (&t)[Q], const bool (&run)[Q],
-                                          const uint32_t (&a)[Q], const uint32_t (&b)[Q], const uint32_t (&key)[Q],
-                                          const Hist& h, uint32_t (&w)[Q]) {
-    DevTable tab[Q];
-    bool act[Q];
-#pragma unroll
-    for (int j = 0; j < Q; j++) {
-        act[j] = run[j] && t[j] >= 0;
-        tab[j] = act[j] ? load_tab(T.tabs, t[j]) : DevTable{};
-        if (run[j] && t[j] < 0) w[j] = verdict(kActPermit, T.slot_noacl);  // nil ACL (:506-508)
-    }
-    eval_q(T, T.blobs, tab, act, a, b, key, w);
-    if (COUNT) {
-#pragma unroll
-        for (int j = 0; j < Q; j++)
-            if (run[j]) h.inc(w[j] & kSlotMask);
-    }
-}
-
-// testConnection (aclengine_mock.go:424-501) of Q connections on resolved end points, each
-// of its up-to-4 evalACL steps in lockstep over the Q connections.
-template <int Q, bool COUNT>
-__device__ __forceinline__ void conn_q(const DevTableSet& T, const End (&es)[Q], const End (&ed)[Q],
-                                       const uint32_t (&src)[Q], const uint32_t (&dst)[Q], const uint32_t (&ksyn)[Q],
-                                       const uint32_t (&kack)[Q], const Hist& h, uint32_t (&out)[Q]) {
-    bool live[Q], srefl[Q], drefl[Q], same[Q], run[Q];
-    uint32_t w[Q];
-    int32_t t[Q];
-#pragma unroll
-    for (int j = 0; j < Q; j++) {
-        live[j] = es[j].ifc >= 0 && ed[j].ifc >= 0;
-        srefl[j] = drefl[j] = false;
-        same[j] = es[j].ifc == ed[j].ifc;
-        w[j] = 0;
-        if (!live[j]) {
-            out[j] = verdict(3u, T.slot_unresolved);
-            if (COUNT) h.inc(T.slot_unresolved);
-        }
-    }
-    // SYN: src interface inbound
-#pragma unroll
-    for (int j = 0; j < Q; j++) t[j] = es[j].tin, run[j] = live[j];
-    eval_step<Q, COUNT>(T, t, run, src, dst, ksyn, h, w);
-#pragma unroll
-    for (int j = 0; j < Q; j++) {
-        if (!run[j]) continue;
-        const uint32_t a = w[j] >> 30;
-        if (a == kActFailure || a == kActDeny) {
-            out[j] = verdict(a == kActFailure ? 3u : 0u, w[j] & kSlotMask);
-            live[j] = false;
-        } else if (a == kActReflect) {
-            srefl[j] = true;
-            drefl[j] = same[j];
-        }
-    }
-    // SYN: dst interface outbound
-#pragma unroll
-    for (int j = 0; j < Q; j++) t[j] = ed[j].tout, run[j] = live[j] && !drefl[j];
-    eval_step<Q, COUNT>(T, t, run, src, dst, ksyn, h, w);
-#pragma unroll
-    for (int j = 0; j < Q; j++) {
-        if (!run[j]) continue;
-        const uint32_t a = w[j] >> 30;
-        if (a == kActFailure || a == kActDeny) {
-            out[j] = verdict(a == kActFailure ? 3u : 0u, w[j] & kSlotMask);
-            live[j] = false;
-        } else if (a == kActReflect) {
-            drefl[j] = true;
-            if (same[j]) srefl[j] = true;
-        }
-    }
-    // SYN-ACK: dst interface inbound
-#pragma unroll
-    for (int j = 0; j < Q; j++) t[j] = ed[j].tin, run[j] = live[j] && !drefl[j];
-    eval_step<Q, COUNT>(T, t, run, dst, src, kack, h, w);
-#pragma unroll
-    for (int j = 0; j < Q; j++) {
-        if (!run[j]) continue;
-        const uint32_t a = w[j] >> 30;
-        if (a == kActFailure || a == kActDeny) {
-            out[j] = verdict(a == kActFailure ? 3u : 1u, w[j] & kSlotMask);
-            live[j] = false;
-        }
-    }
-    // SYN-ACK: src interface outbound
-#pragma unroll
-    for (int j = 0; j < Q; j++) t[j] = es[j].tout, run[j] = live[j] && !srefl[j];
-    eval_step<Q, COUNT>(T, t, run, dst, src, kack, h, w);
-#pragma unroll
-    for (int j = 0; j < Q; j++) {
-        if (!live[j]) continue;
-        const uint32_t a = w[j] >> 30;
-        if (run[j] && (a == kActFailure || a == kActDeny)) out[j] = verdict(a == kActFailure ? 3u : 1u, w[j] & kSlotMask);
-        else out[j] = verdict(2u, w[j] & kSlotMask);  // allowed; slot of the last evaluation
-    }
-}
-
-// Q tuples of one lane, any mode. SINGLE: tab0 is the (uniform) table, its blob at `blobs`.
-template <int MODE, bool COUNT, int Q>
-__device__ __forceinline__ void classify_q(const DevTableSet& T, const uint32_t* blobs, const DevTable& tab0,
-                                           const uint32_t (&s)[Q], const uint32_t (&d)[Q], const uint32_t (&sp)[Q],
-                                           const uint32_t (&dp)[Q], const uint32_t (&pr)[Q], const Hist& h,
-                                           uint32_t (&out)[Q]) {
-    uint32_t key[Q];
-#pragma unroll
-    for (int j = 0; j < Q; j++) key[j] = pkt_key(pr[j], dp[j]);
-    if (MODE == 0) {  // SINGLE
-        DevTable tab[Q];
-        bool act[Q];
-#pragma unroll
-        for (int j = 0; j < Q; j++) tab[j] = tab0, act[j] = true;
-        eval_q(T, blobs, tab, act, s, d, key, out);
-        if (COUNT) {
-#pragma unroll
-            for (int j = 0; j < Q; j++) h.inc(out[j] & kSlotMask);
-        }
-    } else if (MODE == 1) {  // PERPOD: outbound ACL of the interface dst is reached by
-        End e[Q];
-        probe_q(T, d, e);
-        int32_t t[Q];
-        bool run[Q];
-#pragma unroll
-        for (int j = 0; j < Q; j++) {
-            run[j] = e[j].ifc >= 0;
-            t[j] = e[j].tout;
-            if (!run[j]) {
-                out[j] = verdict(kActFailure, T.slot_unresolved);
-                if (COUNT) h.inc(T.slot_unresolved);
-            }
-        }
-        eval_step<Q, COUNT>(T, t, run, s, d, key, h, out);
-    } else {  // CONN
-        uint32_t ips[2 * Q];
-        End e[2 * Q];
-#pragma unroll
-        for (int j = 0; j < Q; j++) ips[j] = s[j], ips[Q + j] = d[j];
-        probe_q(T, ips, e);
-        End es[Q], ed[Q];
-        uint32_t kack[Q];
-#pragma unroll
-        for (int j = 0; j < Q; j++) es[j] = e[j], ed[j] = e[Q + j], kack[j] = pkt_key(pr[j], sp[j]);
-        conn_q<Q, COUNT>(T, es, ed, s, d, key, kack, h, out);
-    }
 }
 
 constexpr int kBlock = 256;
@@ -439,7 +173,8 @@ __device__ __forceinline__ void stream_store(V v, V* p) {
 
 // STAGE (SINGLE mode only): the table's blob (stage_words u32, multiple of 4) is copied into
 // LDS once per workgroup and every lookup of the grid-stride loop reads it from there.
-template <int MODE, bool COUNT, bool VEC, bool STAGE>
+// NODE (PERPOD / CONN): the node classifier; STAGE then copies the node image into LDS.
+template <int MODE, bool COUNT, bool VEC, bool STAGE, bool NODE>
 __global__ __launch_bounds__(kBlock) void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
                                                      const uint32_t* __restrict__ dst,
                                                      const uint16_t* __restrict__ sport,
@@ -453,6 +188,12 @@ __global__ __launch_bounds__(kBlock) void k_classify(DevTableSet T, int32_t t, c
     const bool use_lds = COUNT && T.n_slots <= kLdsHistMax;
     DevTable tab0{};
     const uint32_t* blobs = T.blobs;
+    DevLoader img{T.node.img};
+    if (NODE && STAGE) {
+        const uint4* g = reinterpret_cast<const uint4*>(T.node.img);
+        for (uint32_t i = threadIdx.x; i < stage_words / 4u; i += kBlock) reinterpret_cast<uint4*>(smem)[i] = g[i];
+        img.b = smem;
+    }
     if (MODE == 0) {
         tab0 = load_tab(T.tabs, t);
         if (STAGE) {
@@ -500,7 +241,8 @@ __global__ __launch_bounds__(kBlock) void k_classify(DevTableSet T, int32_t t, c
         const uint32_t sp4[4] = {cur.sp.x & 0xFFFFu, cur.sp.x >> 16, cur.sp.y & 0xFFFFu, cur.sp.y >> 16};
         const uint32_t pr4[4] = {cur.pr & 0xFFu, (cur.pr >> 8) & 0xFFu, (cur.pr >> 16) & 0xFFu, cur.pr >> 24};
         uint32_t o[4];
-        classify_q<MODE, COUNT, 4>(T, blobs, tab0, s4, d4, sp4, dp4, pr4, h, o);
+        if constexpr (NODE) classify_node_q<MODE, COUNT, 4>(T, T.node, img, s4, d4, sp4, dp4, pr4, h, o);
+        else classify_q<MODE, COUNT, 4>(T, blobs, tab0, s4, d4, sp4, dp4, pr4, h, o);
         stream_store(v4u{o[0], o[1], o[2], o[3]}, reinterpret_cast<v4u*>(out + (q << 2)));
         cur = nxt;
         q = qn;
@@ -510,7 +252,8 @@ __global__ __launch_bounds__(kBlock) void k_classify(DevTableSet T, int32_t t, c
         const uint32_t s1[1] = {src[i]}, d1[1] = {dst[i]}, sp1[1] = {MODE == 2 ? (uint32_t)sport[i] : 0u},
                        dp1[1] = {dport[i]}, pr1[1] = {proto[i]};
         uint32_t o[1];
-        classify_q<MODE, COUNT, 1>(T, blobs, tab0, s1, d1, sp1, dp1, pr1, h, o);
+        if constexpr (NODE) classify_node_q<MODE, COUNT, 1>(T, T.node, img, s1, d1, sp1, dp1, pr1, h, o);
+        else classify_q<MODE, COUNT, 1>(T, blobs, tab0, s1, d1, sp1, dp1, pr1, h, o);
         out[i] = o[0];
     }
     if (COUNT && use_lds) {
@@ -638,17 +381,22 @@ __global__ void k_conn_queries(DevTableSet T, const ConnQueryDev* q, uint32_t n,
     const End es[1] = {end(c.src_if)}, ed[1] = {end(c.dst_if)};
     const uint32_t s1[1] = {c.src_ip}, d1[1] = {c.dst_ip}, ks[1] = {c.key_syn}, ka[1] = {c.key_synack};
     uint32_t o[1];
-    conn_q<1, false>(T, es, ed, s1, d1, ks, ka, Hist{nullptr, nullptr}, o);
+    const TabEval<1> ev{T, s1, d1, ks, ka};
+    conn_q<1, false>(T, ev, es, ed, Hist{nullptr, nullptr}, o);
     out[i] = o[0];
 }
 
 // ---- launchers --------------------------------------------------------------------------------
 static uint32_t g_blocks_per_cu = 0;        // 0: as many workgroups per CU as fit (occupancy)
 static uint32_t g_stage_max_words = 16384;  // blobs up to 64 KiB are staged in LDS
+static uint32_t g_node_stage_max_words = 16384;  // node images up to 64 KiB are staged in LDS
+static uint32_t g_node_path = 1;            // PERPOD / CONN through the node classifier when built
 
 int dev_set_tuning(const std::string& key, int value) {
     if (key == "blocks_per_cu" && value >= 0 && value <= 64) g_blocks_per_cu = (uint32_t)value;
     else if (key == "stage_max_words" && value >= 0 && value <= 36864) g_stage_max_words = (uint32_t)value;
+    else if (key == "node_stage_max_words" && value >= 0 && value <= 36864) g_node_stage_max_words = (uint32_t)value;
+    else if (key == "node_path" && (value == 0 || value == 1)) g_node_path = (uint32_t)value;
     else return -1;
     return 0;
 }
@@ -684,27 +432,41 @@ static int grid_resident(K kernel, size_t lds, uint64_t items) {
     return (int)std::max<uint64_t>(1, std::min<uint64_t>(g, (uint64_t)num_cus() * per_cu));
 }
 
+template <int MODE, bool COUNT, bool VEC, bool STAGE, bool NODE>
+static void launch_one(const DevTableSet& T, int t, const uint32_t* src, const uint32_t* dst, const uint16_t* sport,
+                       const uint16_t* dport, const uint8_t* proto, uint64_t n, uint32_t* out,
+                       unsigned long long* counters, hipStream_t st, size_t hist, uint32_t stage, uint64_t items) {
+    auto k = k_classify<MODE, COUNT, VEC, STAGE, NODE>;
+    const size_t lds = hist + (size_t)stage * 4;
+    hipLaunchKernelGGL(k, dim3(grid_resident(k, lds, items)), dim3(kBlock), lds, st, T, t, src, dst, sport, dport,
+                       proto, n, out, counters, stage);
+}
+
 template <int MODE, bool COUNT, bool VEC>
 static void launch_classify(const DevTableSet& T, int t, const uint32_t* src, const uint32_t* dst,
                             const uint16_t* sport, const uint16_t* dport, const uint8_t* proto, uint64_t n,
                             uint32_t* out, unsigned long long* counters, hipStream_t st) {
     const size_t hist = (COUNT && T.n_slots <= kLdsHistMax) ? T.n_slots * 4 : 0;
-    uint32_t stage = 0;
-    if (MODE == 0) {
+    const uint64_t items = VEC ? (n + 3) / 4 : n;
+    if constexpr (MODE == 0) {
         const DevTable& hd = T.host_tabs[t];
         const uint32_t words = T.host_blob_words[t];
-        if (!(hd.fsk & kFlagLinear) && words <= g_stage_max_words) stage = words;
-    }
-    const uint64_t items = VEC ? (n + 3) / 4 : n;
-    if (stage) {
-        auto k = k_classify<MODE, COUNT, VEC, true>;
-        const size_t lds = hist + stage * 4;
-        hipLaunchKernelGGL(k, dim3(grid_resident(k, lds, items)), dim3(kBlock), lds, st, T, t, src, dst, sport, dport,
-                           proto, n, out, counters, stage);
+        if (!(hd.fsk & kFlagLinear) && words && words <= g_stage_max_words)
+            launch_one<MODE, COUNT, VEC, true, false>(T, t, src, dst, sport, dport, proto, n, out, counters, st, hist,
+                                                      words, items);
+        else
+            launch_one<MODE, COUNT, VEC, false, false>(T, t, src, dst, sport, dport, proto, n, out, counters, st,
+                                                       hist, 0, items);
+    } else if (g_node_path && T.node.img) {
+        if (T.node.img_words <= g_node_stage_max_words)
+            launch_one<MODE, COUNT, VEC, true, true>(T, t, src, dst, sport, dport, proto, n, out, counters, st, hist,
+                                                     T.node.img_words, items);
+        else
+            launch_one<MODE, COUNT, VEC, false, true>(T, t, src, dst, sport, dport, proto, n, out, counters, st, hist,
+                                                      0, items);
     } else {
-        auto k = k_classify<MODE, COUNT, VEC, false>;
-        hipLaunchKernelGGL(k, dim3(grid_resident(k, hist, items)), dim3(kBlock), hist, st, T, t, src, dst, sport,
-                           dport, proto, n, out, counters, 0u);
+        launch_one<MODE, COUNT, VEC, false, false>(T, t, src, dst, sport, dport, proto, n, out, counters, st, hist, 0,
+                                                   items);
     }
 }
 

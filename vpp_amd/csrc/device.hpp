@@ -40,6 +40,25 @@ struct DevTable {          // 32 B: two 16-B loads
     uint32_t n_rules;
 };
 
+// Node classifier (fastpath.cpp build_node; PERPOD / CONN modes): every table the node
+// covers evaluated through one IPv4 trie and one L4-key trie shared by all tables, and one
+// cross-table entry per evaluation.
+//   img    u32[]  IPv4 trie (root at word 0, leaf = node IP class) | L4-key trie (leaf = node
+//                 key class) | ipinfo uint2[n_ipc] {interface, tin | tout << 16} | tabinfo
+//                 uint2[T] {cross base, nkc | covered << 31} | kmap u16[T][gk] (local key class)
+//   cross  u32[]  per covered table, [ip class][local key class] -> verdict, or kNodeList |
+//                 first dst record (16 B records, blobwalk.hpp, ending with a match-all one)
+constexpr uint32_t kNodeList = 1u << 29, kNodeRecMask = kNodeList - 1u;
+struct DevNode {
+    const uint32_t* img;   // null: no node classifier (the per-table path runs)
+    const uint32_t* cross;
+    uint32_t img_words;
+    uint32_t ip_s1, key_root, key_k1;
+    uint32_t ipinfo, tabinfo, kmap;  // word offsets in img
+    uint32_t gk;           // node key classes
+    uint32_t n_ipc;        // node IP classes
+};
+
 struct DevTableSet {       // device pointers (valid on the GPU)
     const DevRule* rules;
     const DevTable* tabs;
@@ -55,6 +74,7 @@ struct DevTableSet {       // device pointers (valid on the GPU)
     uint32_t slot_noacl;   // NR + T
     uint32_t slot_unresolved;
     uint32_t n_slots;
+    DevNode node;
     const DevTable* host_tabs;       // host copies (launch decisions; not dereferenced on the GPU)
     const uint32_t* host_blob_words;
 };
@@ -69,12 +89,27 @@ struct HostTableSet {
     std::vector<uint32_t> iphash;
     uint32_t iphash_mask = 0;
     int32_t node_if = -1, node_in = -1, node_out = -1;
+    std::vector<uint32_t> node_img, node_cross;  // empty img: no node classifier
+    DevNode node{};                              // header fields (pointers unset)
 };
 
-// fastpath.cpp: classification blob of one table (false = does not fit the budgets)
+// fastpath.cpp: classification blob of one table (false = does not fit the budgets). When
+// `an` is given it receives the table's class analysis for build_node.
+struct TableAnalysis;
 bool build_fast_table(const DevRule* rules, uint32_t n, uint32_t rule_base, uint32_t default_slot,
-                      std::vector<uint32_t>& blob, uint64_t cross_budget);
+                      std::vector<uint32_t>& blob, uint64_t cross_budget, TableAnalysis** an = nullptr);
+void free_analysis(TableAnalysis* an);
+// fastpath.cpp: the node classifier over the tables with an analysis (null = not covered).
+// pods: {IPv4, interface, inbound table, outbound table} of local pods; node_end: the same for
+// every other address. false = over budget (h.node_img left empty).
+struct NodePod {
+    uint32_t ip;
+    int32_t ifc, tin, tout;
+};
+bool build_node(HostTableSet& h, const std::vector<TableAnalysis*>& an, const std::vector<NodePod>& pods,
+                const NodePod& node_end);
 void set_root_bits_max(uint32_t bits);  // cap of the tries' root stride (4..16)
+void set_node_tuning(uint32_t enable, uint32_t root_bits);
 
 struct GenParams {         // device view of pg_gen_spec
     uint64_t seed, index_base;

@@ -1,7 +1,7 @@
 // Device ACL engine: ACL install semantics + the table compiler.
 #include "engine.hpp"
 
-#include "blobwalk.hpp"
+#include "classify.hpp"
 
 #include <algorithm>
 #include <set>
@@ -147,15 +147,6 @@ int Engine::iface_of(const std::string& name) const {
 
 const DevTableSet* Engine::view() const { return cur ? &dev_view(cur) : nullptr; }
 
-static uint32_t hash_ip(uint32_t ip) {
-    ip ^= ip >> 16;
-    ip *= 0x7feb352du;
-    ip ^= ip >> 15;
-    ip *= 0x846ca68bu;
-    ip ^= ip >> 16;
-    return ip;
-}
-
 int Engine::sync() {
     if (!dirty && cur) return PG_OK;
     if (!compiled) compile();
@@ -212,12 +203,13 @@ void Engine::compile() {
     }
     const uint32_t NR = (uint32_t)h.rules.size();
     h.blob_words.assign(h.tabs.size(), 0);
+    std::vector<TableAnalysis*> an(h.tabs.size(), nullptr);
     for (size_t t = 0; t < h.tabs.size(); t++) {
         DevTable& hdr = h.tabs[t];
         std::vector<uint32_t> blob;
         hdr.dflt = (kActDeny << 30) | (NR + (uint32_t)t);
         if (build_fast_table(h.rules.data() + hdr.rule_base, hdr.n_rules, hdr.rule_base, NR + (uint32_t)t, blob,
-                             1ull << 22)) {
+                             1ull << 22, &an[t])) {
             while (blob.size() % 4) blob.push_back(0);
             hdr.blob_off = (uint32_t)h.blobs.size();
             hdr.fsk = blob[0] | (blob[3] << 8) | (blob[5] << 16);
@@ -283,6 +275,11 @@ void Engine::compile() {
         h.iphash[4 * s + 2] = (uint32_t)e.tin;
         h.iphash[4 * s + 3] = (uint32_t)e.tout;
     }
+    // node classifier for the PERPOD / CONN modes (same end points as the iphash)
+    std::vector<NodePod> np;
+    for (auto& e : ipmap) np.push_back(NodePod{e.ip, e.ifc, e.tin, e.tout});
+    build_node(h, an, np, NodePod{0, h.node_if, h.node_in, h.node_out});
+    for (TableAnalysis* a : an) free_analysis(a);
     compiled = true;
 }
 

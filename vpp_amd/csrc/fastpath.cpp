@@ -111,12 +111,37 @@ uint32_t pick_stride(size_t nb, uint32_t W) {
 bool unconditional(const DevRule& r) { return r.dmask == 0 && r.klo == 0 && r.khi == kKeyMax; }
 bool live(const DevRule& r) { return r.klo <= r.khi; }  // can match a TCP/UDP/OTHER packet
 
+uint32_t g_node_enable = 1;
+uint32_t g_node_root_bits = 12;           // node IPv4 trie root: 2^12 words = 16 KiB
+constexpr uint64_t kNodeCrossBudget = 1ull << 25;  // node cross entries (128 MiB)
+
 }  // namespace
 
+// The classes of one table, kept for the node classifier (cross-product tables only).
+struct TableAnalysis {
+    const DevRule* rules = nullptr;
+    uint32_t rule_base = 0;
+    std::vector<uint64_t> sb;          // src elementary interval starts
+    std::vector<uint32_t> sint_cls;    // their src classes
+    uint32_t nsc = 0;
+    std::vector<uint64_t> kb;          // key segment starts
+    std::vector<uint32_t> kseg_cls;    // their key classes
+    uint32_t nkc = 0;
+    std::vector<uint32_t> cverd;       // [src class][key class] verdict
+    std::vector<std::vector<uint32_t>> clist;  // dst-specific rules in front of it
+};
+
+void free_analysis(TableAnalysis* an) { delete an; }
+
 void set_root_bits_max(uint32_t bits) { g_root_bits_max = std::max<uint32_t>(4, std::min<uint32_t>(16, bits)); }
+void set_node_tuning(uint32_t enable, uint32_t root_bits) {
+    g_node_enable = enable;
+    g_node_root_bits = std::max<uint32_t>(4, std::min<uint32_t>(16, root_bits));
+}
 
 bool build_fast_table(const DevRule* rules, uint32_t n, uint32_t rule_base, uint32_t default_slot,
-                      std::vector<uint32_t>& blob, uint64_t cross_budget) {
+                      std::vector<uint32_t>& blob, uint64_t cross_budget, TableAnalysis** an) {
+    if (an) *an = nullptr;
     blob.assign(16, 0);
     const uint32_t dflt = (kActDeny << 30) | default_slot;
     blob[1] = dflt;
@@ -274,6 +299,20 @@ bool build_fast_table(const DevRule* rules, uint32_t n, uint32_t rule_base, uint
         blob[7] = nkc;
         while (blob.size() % 4) blob.push_back(0);
         blob[6] = (uint32_t)blob.size();
+        if (an) {
+            auto* a = new TableAnalysis();
+            a->rules = rules;
+            a->rule_base = rule_base;
+            a->sb = sb;
+            a->sint_cls = sint_cls;
+            a->nsc = nsc;
+            a->kb = kb;
+            a->kseg_cls = kseg_cls;
+            a->nkc = nkc;
+            a->cverd = cverd;
+            if (lists) a->clist = clist;
+            *an = a;
+        }
         if (!lists) {
             blob[0] = kFlagCross;
             blob.insert(blob.end(), cverd.begin(), cverd.end());
@@ -324,6 +363,167 @@ bool build_fast_table(const DevRule* rules, uint32_t n, uint32_t rule_base, uint
         }
         put_rec(0, 0, 0, kKeyMax, dflt);  // no candidate matched: the table's default deny
     }
+    return true;
+}
+
+// ---- node classifier -------------------------------------------------------------------------
+// One IPv4 partition for the whole node: cut at every covered table's src interval boundary
+// and around every local pod address; elementary intervals with the same end point
+// (interface + its tables) and the same src class in every covered table share a node IP
+// class. Likewise one L4-key partition, node key class -> each table's key class by `kmap`.
+// Then cross[t][ip class][local key class] is table t's cross entry for (its src class of
+// that IP class, key class): an evaluation is two LDS trie walks (shared by every table and
+// both directions of a connection) and one global load.
+bool build_node(HostTableSet& h, const std::vector<TableAnalysis*>& an, const std::vector<NodePod>& pods,
+                const NodePod& node_end) {
+    h.node_img.clear();
+    h.node_cross.clear();
+    h.node = DevNode{};
+    const uint32_t T = (uint32_t)h.tabs.size();
+    if (!g_node_enable || T == 0 || T >= 0xFFFFu) return false;
+    std::vector<uint32_t> cov;
+    for (uint32_t t = 0; t < T; t++)
+        if (an[t] && an[t]->nkc <= 0xFFFFu) cov.push_back(t);
+    if (cov.empty()) return false;
+
+    // IPv4 partition
+    std::vector<uint64_t> gb{0};
+    for (uint32_t t : cov) gb.insert(gb.end(), an[t]->sb.begin(), an[t]->sb.end());
+    if ((uint64_t)h.rules.size() + T + 2 >= kNodeList) return false;  // verdict slots below the list flag
+    std::map<uint32_t, NodePod> by_ip;  // a repeated address: the last pod wins, as in the iphash
+    for (const NodePod& p : pods) by_ip[p.ip] = p;
+    std::vector<NodePod> ps;
+    for (auto& kv : by_ip) ps.push_back(kv.second);
+    for (const NodePod& p : ps) {
+        gb.push_back(p.ip);
+        if ((uint64_t)p.ip + 1 < (1ull << 32)) gb.push_back((uint64_t)p.ip + 1);
+    }
+    std::sort(gb.begin(), gb.end());
+    gb.erase(std::unique(gb.begin(), gb.end()), gb.end());
+    const size_t C = cov.size();
+    std::vector<size_t> at(C, 0);
+    std::unordered_map<std::vector<uint32_t>, uint32_t, VecHash> ipc_of;
+    std::vector<std::vector<uint32_t>> ipc_key;  // class -> {ifc, tin, tout, local src classes...}
+    std::vector<uint32_t> gcls(gb.size());
+    size_t pi = 0;
+    std::vector<uint32_t> key(3 + C);
+    for (size_t k = 0; k < gb.size(); k++) {
+        const uint64_t a = gb[k];
+        while (pi < ps.size() && ps[pi].ip < a) pi++;
+        const NodePod& e = (pi < ps.size() && ps[pi].ip == a) ? ps[pi] : node_end;
+        key[0] = (uint32_t)e.ifc, key[1] = (uint32_t)e.tin, key[2] = (uint32_t)e.tout;
+        for (size_t c = 0; c < C; c++) {
+            const TableAnalysis& A = *an[cov[c]];
+            while (at[c] + 1 < A.sb.size() && A.sb[at[c] + 1] <= a) at[c]++;
+            key[3 + c] = A.sint_cls[at[c]];
+        }
+        auto it = ipc_of.find(key);
+        if (it == ipc_of.end()) {
+            it = ipc_of.emplace(key, (uint32_t)ipc_key.size()).first;
+            ipc_key.push_back(key);
+        }
+        gcls[k] = it->second;
+    }
+    const uint32_t G = (uint32_t)ipc_key.size();
+    uint64_t entries = 0;
+    for (uint32_t t : cov) entries += (uint64_t)G * an[t]->nkc;
+    if (entries > kNodeCrossBudget) return false;
+
+    // L4-key partition
+    std::vector<uint64_t> kb{0};
+    for (uint32_t t : cov) kb.insert(kb.end(), an[t]->kb.begin(), an[t]->kb.end());
+    std::sort(kb.begin(), kb.end());
+    kb.erase(std::unique(kb.begin(), kb.end()), kb.end());
+    std::fill(at.begin(), at.end(), 0);
+    std::unordered_map<std::vector<uint32_t>, uint32_t, VecHash> kc_of;
+    std::vector<std::vector<uint32_t>> kc_key;
+    std::vector<uint32_t> kcls(kb.size());
+    std::vector<uint32_t> kk(C);
+    for (size_t k = 0; k < kb.size(); k++) {
+        for (size_t c = 0; c < C; c++) {
+            const TableAnalysis& A = *an[cov[c]];
+            while (at[c] + 1 < A.kb.size() && A.kb[at[c] + 1] <= kb[k]) at[c]++;
+            kk[c] = A.kseg_cls[at[c]];
+        }
+        auto it = kc_of.find(kk);
+        if (it == kc_of.end()) {
+            it = kc_of.emplace(kk, (uint32_t)kc_key.size()).first;
+            kc_key.push_back(kk);
+        }
+        kcls[k] = it->second;
+    }
+    const uint32_t GK = (uint32_t)kc_key.size();
+
+    // image: tries, ipinfo, tabinfo, kmap
+    std::vector<uint32_t>& img = h.node_img;
+    DevNode& N = h.node;
+    N.ip_s1 = std::min(pick_stride(gb.size(), 32), g_node_root_bits);
+    if (build_trie(img, gb, gcls, 32, N.ip_s1) != 0) return false;
+    N.key_k1 = std::min(pick_stride(kb.size(), 18), g_node_root_bits);
+    N.key_root = build_trie(img, kb, kcls, 18, N.key_k1);
+    while (img.size() % 2) img.push_back(0);
+    N.ipinfo = (uint32_t)img.size();
+    for (uint32_t g = 0; g < G; g++) {
+        const auto& k = ipc_key[g];
+        auto t16 = [](uint32_t t) { return (int32_t)t < 0 ? 0xFFFFu : t; };
+        img.push_back(k[0]);
+        img.push_back(t16(k[1]) | (t16(k[2]) << 16));
+    }
+    N.tabinfo = (uint32_t)img.size();
+    img.resize(img.size() + 2 * (size_t)T, 0);
+    N.kmap = (uint32_t)img.size();
+    img.resize(img.size() + ((size_t)T * GK + 1) / 2, 0);
+    while (img.size() % 4) img.push_back(0);
+    N.gk = GK;
+    N.n_ipc = G;
+    N.img_words = (uint32_t)img.size();
+
+    // cross entries, then the dst records of the pairs with a list
+    std::vector<uint32_t>& X = h.node_cross;
+    X.reserve(entries + 16);
+    std::vector<uint32_t> recs;
+    const size_t rec0 = (entries + 3) & ~(uint64_t)3;
+    for (size_t c = 0; c < C; c++) {
+        const uint32_t t = cov[c];
+        const TableAnalysis& A = *an[t];
+        img[N.tabinfo + 2 * t] = (uint32_t)X.size();
+        img[N.tabinfo + 2 * t + 1] = A.nkc | 0x80000000u;
+        for (uint32_t g = 0; g < GK; g++) {
+            const uint32_t ki = t * GK + g;
+            img[N.kmap + ki / 2] |= kc_key[g][c] << ((ki & 1u) * 16u);
+        }
+        std::vector<uint32_t> first(A.clist.empty() ? 0 : A.cverd.size(), 0xFFFFFFFFu);
+        for (uint32_t g = 0; g < G; g++) {
+            const uint32_t sc = ipc_key[g][3 + c];
+            for (uint32_t lk = 0; lk < A.nkc; lk++) {
+                const size_t e = (size_t)sc * A.nkc + lk;
+                if (A.clist.empty() || A.clist[e].empty()) {
+                    X.push_back(A.cverd[e]);
+                    continue;
+                }
+                if (first[e] == 0xFFFFFFFFu) {
+                    const uint64_t ri = (rec0 + recs.size()) / 4;
+                    if (ri >= kNodeRecMask) return false;
+                    first[e] = (uint32_t)ri;
+                    for (uint32_t r : A.clist[e]) {
+                        const DevRule& R = A.rules[r];
+                        recs.push_back(R.dnet);
+                        recs.push_back((uint32_t)__builtin_popcount(R.dmask) << 18);
+                        recs.push_back(kKeyMax);
+                        recs.push_back(((R.act & 3u) << 30) | (A.rule_base + r));
+                    }
+                    recs.push_back(0);
+                    recs.push_back(0);
+                    recs.push_back(kKeyMax);
+                    recs.push_back(A.cverd[e]);
+                }
+                X.push_back(kNodeList | first[e]);
+            }
+        }
+    }
+    X.resize(rec0, 0);
+    X.insert(X.end(), recs.begin(), recs.end());
+    if (X.empty()) X.resize(4, 0);
     return true;
 }
 

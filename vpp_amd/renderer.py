@@ -253,6 +253,31 @@ class Engine:
         self._ck(lib.pg_debug_walk_blob(self.h, _b(acl_name), p(a[0]), p(a[1]), p(a[2]), p(a[3]), n, p(out)))
         return out
 
+    def debug_classify_host(self, mode, table_id, src, dst, sport, dport, proto, counters=False, node=True):
+        """TESTS ONLY: pg_classify's per-tuple code run on the host (pg_debug_classify_host).
+        -> verdict words (u32), and the u64 hit counters when ``counters``."""
+        import numpy as np
+        n = len(src)
+        a = [np.ascontiguousarray(x, dt) for x, dt in ((src, np.uint32), (dst, np.uint32), (sport, np.uint16),
+                                                       (dport, np.uint16), (proto, np.uint8))]
+        p = lambda x: x.ctypes.data_as(C.c_void_p)
+        t = _capi.pg_tuple_soa(p(a[0]), p(a[1]), p(a[2]), p(a[3]), p(a[4]))
+        out = np.empty(n, np.uint32)
+        cnt = np.zeros(self.num_counter_slots(), np.uint64) if counters else None
+        self._ck(lib.pg_debug_classify_host(self.h, mode, table_id, C.byref(t), n, p(out),
+                                            p(cnt) if counters else None, int(node)))
+        return (out, cnt) if counters else out
+
+    def node_stats(self):
+        """node classifier size {ip_classes, key_classes, image_bytes, cross_bytes}, or None."""
+        a, b = C.c_uint32(), C.c_uint32()
+        c, d = C.c_uint64(), C.c_uint64()
+        rc = lib.pg_node_stats(self.h, C.byref(a), C.byref(b), C.byref(c), C.byref(d))
+        if rc == -2:  # PG_ENOENT
+            return None
+        self._ck(rc)
+        return {"ip_classes": a.value, "key_classes": b.value, "image_bytes": c.value, "cross_bytes": d.value}
+
     def slot_of_rule(self, tid, idx):
         """counter slot of rule ``idx`` of table ``tid`` (idx -1: the table's default deny)."""
         base, n, dflt = self.table_info(tid)
