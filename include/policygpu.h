@@ -144,7 +144,8 @@ pg_ctx* pg_create(int hip_device);
  * afterwards), "node_root_bits" (its IPv4 / key trie root stride cap, default 12),
  * "node_path" (1/0: classify PERPOD / CONN through the node classifier when it exists,
  * default 1; 0 = per-table blobs and the IP hash), "node_stage_max_words" (largest node
- * image staged in LDS, default 16384) */
+ * image staged in LDS, default 16384), "block_stage" (workgroup size of LDS-staged
+ * classify launches: 256, 512 or 1024; default 0 = per mode) */
 int pg_set_tuning(const char* key, int value);
 void pg_destroy(pg_ctx* ctx);
 const char* pg_last_error(const pg_ctx* ctx);
@@ -208,10 +209,11 @@ int pg_debug_walk_blob(pg_ctx* ctx, const char* acl_name, const uint32_t* src, c
                        const uint16_t* dst_port, const uint8_t* proto, uint64_t n, uint32_t* out);
 /* TESTS ONLY -- never on the classify path: pg_classify's per-tuple code (classify.hpp, the
  * same templates the kernels instantiate) run on the host over host tuples, any mode, with
- * optional host u64 counters; node = 1 uses the node classifier when it exists, 0 the
- * per-table path. Does not touch the device. */
+ * optional host u64 counters. flags: bit 0 = node classifier when it exists (else the
+ * per-table path), bit 1 = the predicated trie walks the kernels use on LDS-staged images
+ * (else the branching ones they use on HBM-resident ones). Does not touch the device. */
 int pg_debug_classify_host(pg_ctx* ctx, int mode, int table_id, const pg_tuple_soa* tuples, uint64_t n,
-                           uint32_t* out, uint64_t* counters, int node);
+                           uint32_t* out, uint64_t* counters, int flags);
 /* node classifier (PERPOD / CONN) size: IPv4 classes, L4-key classes, LDS image bytes,
  * cross-table bytes; PG_ENOENT when it was not built */
 int pg_node_stats(pg_ctx* ctx, uint32_t* ip_classes, uint32_t* key_classes, uint64_t* image_bytes,

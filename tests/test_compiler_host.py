@@ -26,6 +26,9 @@ def engine_with(rules_by_name):
 def check(e, name, rules, tup):
     src, dst, sport, dport, proto = tup
     got = e.debug_walk(name, src, dst, dport, proto)
+    for pred in (True, False):  # pg_classify's SINGLE-mode code, LDS (predicated) and HBM walks
+        host = e.debug_classify_host(0, e.table_id(name), src, dst, sport, dport, proto, pred=pred)
+        assert np.array_equal(host, got)
     a, i = fast.eval_acl(fast.OraACL(rules), src, dst, dport, proto)
     names = e.ACLNames()
     base = sum(len(e.GetACLByName(n)["rules"]) for n in names[:names.index(name)])

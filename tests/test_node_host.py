@@ -75,6 +75,10 @@ def check(e, local, tup, expect_node=True):
     act, slot = wd.perpod(src, dst, dport, proto, threads=4)
     pn, cpn = e.debug_classify_host(MODE_PERPOD, -1, *tup, counters=True, node=True)
     pt, cpt = e.debug_classify_host(MODE_PERPOD, -1, *tup, counters=True, node=False)
+    for node in (True, False):  # the branching walks (HBM-resident images) too
+        assert np.array_equal(e.debug_classify_host(MODE_PERPOD, -1, *tup, node=node, pred=False), pn)
+        assert np.array_equal(e.debug_classify_host(MODE_CONN, -1, *tup, node=node, pred=False),
+                              e.debug_classify_host(MODE_CONN, -1, *tup, node=node))
     assert np.array_equal(pn, pt)
     assert np.array_equal(cpn, cpt)
     assert np.array_equal(pn >> 30, act.astype(np.uint32)), np.nonzero((pn >> 30) != act)[0][:8]

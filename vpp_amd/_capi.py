@@ -139,4 +139,5 @@ def load(path=LIB_PATH):
     return lib
 
 
-lib = load()
+# VPP_AMD_LIB: load an A/B build of the same library (tools/sweep.py); default the in-tree build
+lib = load(os.environ.get("VPP_AMD_LIB", LIB_PATH))

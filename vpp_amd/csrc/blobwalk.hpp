@@ -50,7 +50,10 @@ PG_HD bool rec_match(const W4& r, uint32_t dst, uint32_t key) {
 
 // on[j]: tuple j is walked (table present, not LINEAR, key < kWalkKeyLimit). w[j] is only
 // written for those.
-template <class L, int Q>
+// PRED: the trie descent issues a load for every tuple at every level (a finished tuple
+// re-reads word 0) instead of branching per tuple: cheaper when the blob is in LDS, where a
+// wasted read costs little and per-lane branches cost exec-mask juggling.
+template <bool PRED = false, class L, int Q>
 PG_HD void blob_walk(const L (&ld)[Q], const BlobTab (&tb)[Q], const bool (&on)[Q], const uint32_t (&src)[Q],
                      const uint32_t (&dst)[Q], const uint32_t (&key)[Q], uint32_t (&w)[Q]) {
     uint32_t es[Q], ek[Q], ss[Q], sk[Q];
@@ -75,6 +78,19 @@ PG_HD void blob_walk(const L (&ld)[Q], const BlobTab (&tb)[Q], const bool (&on)[
         if (!more) break;
         PG_UNROLL
         for (int j = 0; j < Q; j++) {
+            if (PRED) {
+                const bool ds = !(es[j] & kLeaf), dk = !(ek[j] & kLeaf);
+                const uint32_t ts = ss[j] < 8u ? ss[j] : 8u, tk = sk[j] < 8u ? sk[j] : 8u;
+                const uint32_t ns = ss[j] - ts, nk = sk[j] - tk;
+                const uint32_t is = ds ? es[j] + ((src[j] >> ns) & ((1u << ts) - 1u)) : 0u;
+                const uint32_t ik = dk ? ek[j] + ((key[j] >> nk) & ((1u << tk) - 1u)) : 0u;
+                const uint32_t vs = ld[j].u32(is), vk = ld[j].u32(ik);
+                es[j] = ds ? vs : es[j];
+                ek[j] = dk ? vk : ek[j];
+                ss[j] = ds ? ns : ss[j];
+                sk[j] = dk ? nk : sk[j];
+                continue;
+            }
             if (!(es[j] & kLeaf)) {
                 const uint32_t st = ss[j] < 8u ? ss[j] : 8u;
                 ss[j] -= st;

@@ -507,7 +507,7 @@ DevTableSet host_view(const HostTableSet& h) {
     return v;
 }
 
-template <int MODE, int Q>
+template <int MODE, int Q, bool PRED>
 void host_q(const DevTableSet& T, bool node, int table_id, const pg_tuple_soa* t, uint64_t i, uint32_t* out,
             const Hist& h) {
     uint32_t s[Q], d[Q], sp[Q], dp[Q], pr[Q], o[Q];
@@ -516,20 +516,26 @@ void host_q(const DevTableSet& T, bool node, int table_id, const pg_tuple_soa* t
         sp[j] = MODE == 2 ? t->src_port[i + j] : 0u;
     }
     if constexpr (MODE == 0) {
-        classify_q<0, true, Q>(T, T.blobs, load_tab(T.tabs, table_id), s, d, sp, dp, pr, h, o);
+        classify_q<0, true, Q, PRED>(T, T.blobs, load_tab(T.tabs, table_id), s, d, sp, dp, pr, h, o);
     } else {
-        if (node) classify_node_q<MODE, true, Q>(T, T.node, DevLoader{T.node.img}, s, d, sp, dp, pr, h, o);
-        else classify_q<MODE, true, Q>(T, T.blobs, DevTable{}, s, d, sp, dp, pr, h, o);
+        if (node) classify_node_q<MODE, true, Q, PRED>(T, T.node, DevLoader{T.node.img}, s, d, sp, dp, pr, h, o);
+        else classify_q<MODE, true, Q, PRED>(T, T.blobs, DevTable{}, s, d, sp, dp, pr, h, o);
     }
     for (int j = 0; j < Q; j++) out[i + j] = o[j];
 }
 
-template <int MODE>
+template <int MODE, bool PRED>
 void host_classify(const DevTableSet& T, bool node, int table_id, const pg_tuple_soa* t, uint64_t n, uint32_t* out,
                    const Hist& h) {
     const uint64_t nq = n & ~(uint64_t)3;  // the kernels' quads, then one tuple at a time
-    for (uint64_t i = 0; i < nq; i += 4) host_q<MODE, 4>(T, node, table_id, t, i, out, h);
-    for (uint64_t i = nq; i < n; i++) host_q<MODE, 1>(T, node, table_id, t, i, out, h);
+    for (uint64_t i = 0; i < nq; i += 4) host_q<MODE, 4, PRED>(T, node, table_id, t, i, out, h);
+    for (uint64_t i = nq; i < n; i++) host_q<MODE, 1, PRED>(T, node, table_id, t, i, out, h);
+}
+template <int MODE>
+void host_classify(const DevTableSet& T, bool node, bool pred, int table_id, const pg_tuple_soa* t, uint64_t n,
+                   uint32_t* out, const Hist& h) {
+    if (pred) host_classify<MODE, true>(T, node, table_id, t, n, out, h);
+    else host_classify<MODE, false>(T, node, table_id, t, n, out, h);
 }
 }  // namespace
 
@@ -547,11 +553,11 @@ int pg_debug_classify_host(pg_ctx* ctx, int mode, int table_id, const pg_tuple_s
     if (n == 0) return PG_OK;
     if (!out || !t->src_ip || !t->dst_ip || !t->dst_port || !t->proto || (mode == PG_MODE_CONN && !t->src_port))
         return fail(ctx, PG_EINVAL, "missing tuple field");
-    const bool use_node = node && T.node.img != nullptr;
+    const bool use_node = (node & 1) && T.node.img != nullptr, pred = (node & 2) != 0;
     const Hist h{nullptr, (unsigned long long*)counters};
-    if (mode == 0) host_classify<0>(T, false, table_id, t, n, out, h);
-    else if (mode == 1) host_classify<1>(T, use_node, table_id, t, n, out, h);
-    else host_classify<2>(T, use_node, table_id, t, n, out, h);
+    if (mode == 0) host_classify<0>(T, false, pred, table_id, t, n, out, h);
+    else if (mode == 1) host_classify<1>(T, use_node, pred, table_id, t, n, out, h);
+    else host_classify<2>(T, use_node, pred, table_id, t, n, out, h);
     return PG_OK;
     GUARD_END(ctx)
 }

@@ -88,7 +88,7 @@ PG_HD DevTable load_tab(const DevTable* tabs, int32_t t) {
 // evalACL of Q tuples against their tables' per-table blobs, in lockstep.
 // act[j]: evaluate tuple j against tab[j]; blobs: base the tables' blob_off is relative to
 // (the global blob array, or the LDS copy of a staged table).
-template <int Q>
+template <bool PRED = false, int Q>
 PG_HD void eval_q(const DevTableSet& T, const uint32_t* blobs, const DevTable (&tab)[Q], const bool (&act)[Q],
                   const uint32_t (&src)[Q], const uint32_t (&dst)[Q], const uint32_t (&key)[Q], uint32_t (&w)[Q]) {
     DevLoader ld[Q];
@@ -100,7 +100,7 @@ PG_HD void eval_q(const DevTableSet& T, const uint32_t* blobs, const DevTable (&
         tb[j] = BlobTab{tab[j].fsk, tab[j].dflt, tab[j].kroot, tab[j].xoff, tab[j].nkc};
         on[j] = act[j] && !(tab[j].fsk & kFlagLinear) && key[j] < kWalkKeyLimit;
     }
-    blob_walk(ld, tb, on, src, dst, key, w);
+    blob_walk<PRED>(ld, tb, on, src, dst, key, w);
     PG_UNROLL
     for (int j = 0; j < Q; j++)
         if (act[j] && !on[j])
@@ -186,8 +186,9 @@ struct TabEval {
 // table per evaluation, cross[tabinfo[t].base + ipclass * nkc_t + kmap[t][keyclass]]: a
 // verdict, or (kNodeList) the first of the dst records to test. Tables the node does not
 // cover, LINEAR tables and ANY-protocol packets take the per-table path.
-// Q trie lookups in lockstep (root stride s1 over a W-bit address, then 8-bit strides)
-template <class L, int Q>
+// Q trie lookups in lockstep (root stride s1 over a W-bit address, then 8-bit strides).
+// PRED: one load per tuple per level, no per-tuple branches (LDS images).
+template <bool PRED, class L, int Q>
 PG_HD void node_trie_q(const L& ld, uint32_t root, uint32_t s1, uint32_t W, const uint32_t (&a)[Q], uint32_t (&c)[Q]) {
     uint32_t sh[Q], e[Q];
     PG_UNROLL
@@ -202,6 +203,14 @@ PG_HD void node_trie_q(const L& ld, uint32_t root, uint32_t s1, uint32_t W, cons
         if (!more) break;
         PG_UNROLL
         for (int j = 0; j < Q; j++) {
+            if (PRED) {
+                const bool d = !(e[j] & kLeaf);
+                const uint32_t st = sh[j] < 8u ? sh[j] : 8u, ns = sh[j] - st;
+                const uint32_t v = ld.u32(d ? e[j] + ((a[j] >> ns) & ((1u << st) - 1u)) : 0u);
+                e[j] = d ? v : e[j];
+                sh[j] = d ? ns : sh[j];
+                continue;
+            }
             if (e[j] & kLeaf) continue;
             const uint32_t st = sh[j] < 8u ? sh[j] : 8u;
             sh[j] -= st;
@@ -220,7 +229,13 @@ PG_HD End node_end(const L& img, const DevNode& N, uint32_t ipc) {
     return End{(int32_t)v.x, tin == 0xFFFFu ? -1 : (int32_t)tin, tout == 0xFFFFu ? -1 : (int32_t)tout};
 }
 
-template <class L, int Q>
+struct NoHook {
+    PG_HD void operator()() const {}
+};
+
+// H: called once per lane, right after the first evaluation's cross-entry loads are issued
+// (the kernels issue the next quad's stream loads there; see device.hip PG_PREFETCH)
+template <class L, int Q, class H = NoHook>
 struct NodeEval {
     const DevTableSet& T;
     const DevNode& N;
@@ -233,6 +248,8 @@ struct NodeEval {
     const uint32_t (&cd)[Q];  // node IP class of dst
     const uint32_t (&gsyn)[Q];  // node key class of the SYN key
     const uint32_t (&gack)[Q];
+    const H& hook;
+    bool* hooked;
     PG_HD void operator()(const int32_t (&t)[Q], const bool (&act)[Q], bool rev, uint32_t (&w)[Q]) const {
         const DevLoader X{N.cross};
         const uint32_t(&a)[Q] = rev ? dst : src;
@@ -260,10 +277,23 @@ struct NodeEval {
         for (int j = 0; j < Q; j++) {
             pend[j] = false;
             if (!on[j]) continue;
-            const uint32_t e = X.u32(pos[j]);
-            w[j] = e;
-            pend[j] = (e & kNodeList) != 0u;
-            pos[j] = (e & kNodeRecMask) << 2;
+            w[j] = X.u32(pos[j]);
+        }
+        if (!*hooked) {
+            *hooked = true;
+#if defined(__HIP_DEVICE_COMPILE__)
+            __builtin_amdgcn_sched_barrier(0);
+#endif
+            hook();
+#if defined(__HIP_DEVICE_COMPILE__)
+            __builtin_amdgcn_sched_barrier(0);
+#endif
+        }
+        PG_UNROLL
+        for (int j = 0; j < Q; j++) {
+            if (!on[j]) continue;
+            pend[j] = (w[j] & kNodeList) != 0u;
+            pos[j] = (w[j] & kNodeRecMask) << 2;
         }
         // dst records until the first match (every list ends with a match-all record)
         for (;;) {
@@ -396,7 +426,7 @@ PG_HD void conn_q(const DevTableSet& T, const EV& ev, const End (&es)[Q], const 
 
 // Q tuples of one lane, any mode, per-table path. SINGLE: tab0 is the (uniform) table, its
 // blob at `blobs`.
-template <int MODE, bool COUNT, int Q>
+template <int MODE, bool COUNT, int Q, bool PRED = false>
 PG_HD void classify_q(const DevTableSet& T, const uint32_t* blobs, const DevTable& tab0, const uint32_t (&s)[Q],
                       const uint32_t (&d)[Q], const uint32_t (&sp)[Q], const uint32_t (&dp)[Q],
                       const uint32_t (&pr)[Q], const Hist& h, uint32_t (&out)[Q]) {
@@ -408,7 +438,7 @@ PG_HD void classify_q(const DevTableSet& T, const uint32_t* blobs, const DevTabl
         bool act[Q];
         PG_UNROLL
         for (int j = 0; j < Q; j++) tab[j] = tab0, act[j] = true;
-        eval_q(T, blobs, tab, act, s, d, key, out);
+        eval_q<PRED>(T, blobs, tab, act, s, d, key, out);
         if (COUNT) {
             PG_UNROLL
             for (int j = 0; j < Q; j++) h.inc(out[j] & kSlotMask);
@@ -446,10 +476,10 @@ PG_HD void classify_q(const DevTableSet& T, const uint32_t* blobs, const DevTabl
 
 // Q tuples of one lane, PERPOD / CONN, node path. `img` reads the node image (LDS copy or
 // global memory).
-template <int MODE, bool COUNT, int Q, class L>
+template <int MODE, bool COUNT, int Q, bool PRED = false, class L, class H = NoHook>
 PG_HD void classify_node_q(const DevTableSet& T, const DevNode& N, const L& img, const uint32_t (&s)[Q],
                            const uint32_t (&d)[Q], const uint32_t (&sp)[Q], const uint32_t (&dp)[Q],
-                           const uint32_t (&pr)[Q], const Hist& h, uint32_t (&out)[Q]) {
+                           const uint32_t (&pr)[Q], const Hist& h, uint32_t (&out)[Q], const H& hook = H()) {
     uint32_t key[Q], kack[Q];
     PG_UNROLL
     for (int j = 0; j < Q; j++) key[j] = pkt_key(pr[j], dp[j]), kack[j] = MODE == 2 ? pkt_key(pr[j], sp[j]) : key[j];
@@ -457,7 +487,7 @@ PG_HD void classify_node_q(const DevTableSet& T, const DevNode& N, const L& img,
     uint32_t ips[2 * Q], ipc[2 * Q];
     PG_UNROLL
     for (int j = 0; j < Q; j++) ips[j] = s[j], ips[Q + j] = d[j];
-    node_trie_q(img, 0u, N.ip_s1, 32u, ips, ipc);
+    node_trie_q<PRED>(img, 0u, N.ip_s1, 32u, ips, ipc);
     uint32_t cs[Q], cd[Q], gs[Q], ga[Q];
     if (MODE == 2) {
         uint32_t keys[2 * Q], kc[2 * Q];
@@ -466,20 +496,21 @@ PG_HD void classify_node_q(const DevTableSet& T, const DevNode& N, const L& img,
             keys[j] = key[j] < kWalkKeyLimit ? key[j] : 0u;
             keys[Q + j] = kack[j] < kWalkKeyLimit ? kack[j] : 0u;
         }
-        node_trie_q(img, N.key_root, N.key_k1, 18u, keys, kc);
+        node_trie_q<PRED>(img, N.key_root, N.key_k1, 18u, keys, kc);
         PG_UNROLL
         for (int j = 0; j < Q; j++) gs[j] = kc[j], ga[j] = kc[Q + j];
     } else {
         uint32_t keys[Q];
         PG_UNROLL
         for (int j = 0; j < Q; j++) keys[j] = key[j] < kWalkKeyLimit ? key[j] : 0u;
-        node_trie_q(img, N.key_root, N.key_k1, 18u, keys, gs);
+        node_trie_q<PRED>(img, N.key_root, N.key_k1, 18u, keys, gs);
         PG_UNROLL
         for (int j = 0; j < Q; j++) ga[j] = gs[j];
     }
     PG_UNROLL
     for (int j = 0; j < Q; j++) cs[j] = ipc[j], cd[j] = ipc[Q + j];
-    const NodeEval<L, Q> ev{T, N, img, s, d, key, kack, cs, cd, gs, ga};
+    bool hooked = false;
+    const NodeEval<L, Q, H> ev{T, N, img, s, d, key, kack, cs, cd, gs, ga, hook, &hooked};
     if (MODE == 1) {
         int32_t t[Q];
         bool run[Q];
@@ -500,6 +531,7 @@ PG_HD void classify_node_q(const DevTableSet& T, const DevNode& N, const L& img,
         for (int j = 0; j < Q; j++) es[j] = node_end(img, N, cs[j]), ed[j] = node_end(img, N, cd[j]);
         conn_q<Q, COUNT>(T, ev, es, ed, h, out);
     }
+    if (!hooked) hook();  // no evaluation ran in this lane
 }
 
 }  // namespace pg

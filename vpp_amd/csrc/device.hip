@@ -174,8 +174,55 @@ __device__ __forceinline__ void stream_store(V v, V* p) {
 // STAGE (SINGLE mode only): the table's blob (stage_words u32, multiple of 4) is copied into
 // LDS once per workgroup and every lookup of the grid-stride loop reads it from there.
 // NODE (PERPOD / CONN): the node classifier; STAGE then copies the node image into LDS.
-template <int MODE, bool COUNT, bool VEC, bool STAGE, bool NODE>
-__global__ __launch_bounds__(kBlock) void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
+//
+// Stream pipelining (PG_PREFETCH): 1 = the next group's loads are issued at the top of each
+// iteration; 2 = (NODE) issued right after the first cross-entry gather of the iteration, so
+// waiting for that gather does not also wait for them (vmcnt retires in issue order); 0 = none;
+// -1 (default) = per mode: none for SINGLE (all lookups in LDS, occupancy hides the stream),
+// top-of-iteration for PERPOD / CONN (tools/sweep.py A/B on MI355X).
+#ifndef PG_PREFETCH
+#define PG_PREFETCH -1
+#endif
+#ifndef PG_PROBE_STREAM  // measurement build only: the streams with no classification
+#define PG_PROBE_STREAM 0
+#endif
+#ifndef PG_PRED  // predicated (branch-free) trie walks on LDS-staged images (A/B: slower)
+#define PG_PRED 0
+#endif
+#ifndef PG_TPL  // tuples per lane per loop iteration (4 or 8)
+#define PG_TPL 4
+#endif
+
+// NW consecutive u32 of a stream with the widest loads / stores (NW = 1, 2, 4, 8)
+template <int NW>
+struct Words {
+    uint32_t w[NW];
+};
+template <int NW>
+__device__ __forceinline__ Words<NW> ld_words(const uint32_t* p) {
+    Words<NW> r;
+    if constexpr (NW == 1) {
+        r.w[0] = stream_load(p);
+    } else if constexpr (NW == 2) {
+        const v2u v = stream_load(reinterpret_cast<const v2u*>(p));
+        r.w[0] = v.x, r.w[1] = v.y;
+    } else {
+#pragma unroll
+        for (int k = 0; k < NW / 4; k++) {
+            const v4u v = stream_load(reinterpret_cast<const v4u*>(p) + k);
+            r.w[4 * k] = v.x, r.w[4 * k + 1] = v.y, r.w[4 * k + 2] = v.z, r.w[4 * k + 3] = v.w;
+        }
+    }
+    return r;
+}
+template <int NW>
+__device__ __forceinline__ void st_words(const Words<NW>& v, uint32_t* p) {
+#pragma unroll
+    for (int k = 0; k < NW / 4; k++)
+        stream_store(v4u{v.w[4 * k], v.w[4 * k + 1], v.w[4 * k + 2], v.w[4 * k + 3]}, reinterpret_cast<v4u*>(p) + k);
+}
+template <int MODE, bool COUNT, bool VEC, bool STAGE, bool NODE, int BS>
+__global__ __launch_bounds__(BS) void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
                                                      const uint32_t* __restrict__ dst,
                                                      const uint16_t* __restrict__ sport,
                                                      const uint16_t* __restrict__ dport,
@@ -191,74 +238,93 @@ __global__ __launch_bounds__(kBlock) void k_classify(DevTableSet T, int32_t t, c
     DevLoader img{T.node.img};
     if (NODE && STAGE) {
         const uint4* g = reinterpret_cast<const uint4*>(T.node.img);
-        for (uint32_t i = threadIdx.x; i < stage_words / 4u; i += kBlock) reinterpret_cast<uint4*>(smem)[i] = g[i];
+        for (uint32_t i = threadIdx.x; i < stage_words / 4u; i += BS) reinterpret_cast<uint4*>(smem)[i] = g[i];
         img.b = smem;
     }
     if (MODE == 0) {
         tab0 = load_tab(T.tabs, t);
         if (STAGE) {
             const uint4* g = reinterpret_cast<const uint4*>(T.blobs + tab0.blob_off);
-            for (uint32_t i = threadIdx.x; i < stage_words / 4u; i += kBlock) reinterpret_cast<uint4*>(smem)[i] = g[i];
+            for (uint32_t i = threadIdx.x; i < stage_words / 4u; i += BS) reinterpret_cast<uint4*>(smem)[i] = g[i];
             blobs = smem;
             tab0.blob_off = 0;
         }
     }
     if (COUNT && use_lds) {
-        for (uint32_t i = threadIdx.x; i < T.n_slots; i += kBlock) hist[i] = 0;
+        for (uint32_t i = threadIdx.x; i < T.n_slots; i += BS) hist[i] = 0;
         h.lds = hist;
     }
     if (STAGE || (COUNT && use_lds)) __syncthreads();
-    const uint64_t stride = (uint64_t)gridDim.x * kBlock;
-    const uint64_t first = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    // full quads: software-pipelined -- the next quad's 44 bytes are in flight while this
-    // quad is classified (16-B src/dst, 8-B ports, 4-B protocols per lane, coalesced)
-    const uint64_t nfull = VEC ? (n >> 2) : 0;
-    struct Quad {
-        v4u s, d;
-        v2u dp, sp;
-        uint32_t pr;
+    const uint64_t stride = (uint64_t)gridDim.x * BS;
+    const uint64_t first = (uint64_t)blockIdx.x * BS + threadIdx.x;
+    // full groups of P tuples per lane (P = PG_TPL): SoA fields read with 16/8/4-byte loads per
+    // lane (coalesced, non-temporal); prefetch 1/2: the next group's loads are in flight
+    // while this group is classified
+    constexpr int P = PG_TPL;
+    const uint64_t nfull = VEC ? (n / P) : 0;
+    struct Group {
+        Words<P> s, d;
+        Words<P / 2> dp, sp;
+        Words<P / 4> pr;
     };
     auto load = [&](uint64_t q) {
-        Quad x;
-        const uint64_t i0 = q << 2;
-        x.s = stream_load(reinterpret_cast<const v4u*>(src + i0));
-        x.d = stream_load(reinterpret_cast<const v4u*>(dst + i0));
-        x.dp = stream_load(reinterpret_cast<const v2u*>(dport + i0));
-        x.pr = stream_load(reinterpret_cast<const uint32_t*>(proto + i0));
-        x.sp = MODE == 2 ? stream_load(reinterpret_cast<const v2u*>(sport + i0)) : v2u{0u, 0u};
+        Group x;
+        const uint64_t i0 = q * P;
+        x.s = ld_words<P>(src + i0);
+        x.d = ld_words<P>(dst + i0);
+        x.dp = ld_words<P / 2>(reinterpret_cast<const uint32_t*>(dport + i0));
+        x.pr = ld_words<P / 4>(reinterpret_cast<const uint32_t*>(proto + i0));
+        if (MODE == 2) x.sp = ld_words<P / 2>(reinterpret_cast<const uint32_t*>(sport + i0));
+        else x.sp = Words<P / 2>{};
         return x;
     };
     uint64_t q = first;
-    Quad cur;
-    if (q < nfull) cur = load(q);
+    Group cur;
+    constexpr int PF = PG_PREFETCH >= 0 ? PG_PREFETCH : (MODE == 0 ? 0 : 1);
+    if (PF && q < nfull) cur = load(q);
     while (q < nfull) {
         const uint64_t qn = q + stride;
-        Quad nxt = cur;
-        if (qn < nfull) nxt = load(qn);
-        const uint32_t s4[4] = {cur.s.x, cur.s.y, cur.s.z, cur.s.w};
-        const uint32_t d4[4] = {cur.d.x, cur.d.y, cur.d.z, cur.d.w};
-        const uint32_t dp4[4] = {cur.dp.x & 0xFFFFu, cur.dp.x >> 16, cur.dp.y & 0xFFFFu, cur.dp.y >> 16};
-        const uint32_t sp4[4] = {cur.sp.x & 0xFFFFu, cur.sp.x >> 16, cur.sp.y & 0xFFFFu, cur.sp.y >> 16};
-        const uint32_t pr4[4] = {cur.pr & 0xFFu, (cur.pr >> 8) & 0xFFu, (cur.pr >> 16) & 0xFFu, cur.pr >> 24};
-        uint32_t o[4];
-        if constexpr (NODE) classify_node_q<MODE, COUNT, 4>(T, T.node, img, s4, d4, sp4, dp4, pr4, h, o);
-        else classify_q<MODE, COUNT, 4>(T, blobs, tab0, s4, d4, sp4, dp4, pr4, h, o);
-        stream_store(v4u{o[0], o[1], o[2], o[3]}, reinterpret_cast<v4u*>(out + (q << 2)));
+        Group nxt = cur;
+        if (!PF) cur = load(q);
+        const bool late = NODE && PF == 2;
+        if (PF && !late && qn < nfull) nxt = load(qn);
+        [[maybe_unused]] auto hook = [&]() {
+            if (late && qn < nfull) nxt = load(qn);
+        };
+        uint32_t sv[P], dv[P], spv[P], dpv[P], prv[P], o[P];
+#pragma unroll
+        for (int j = 0; j < P; j++) {
+            sv[j] = cur.s.w[j];
+            dv[j] = cur.d.w[j];
+            dpv[j] = (cur.dp.w[j / 2] >> (16 * (j & 1))) & 0xFFFFu;
+            spv[j] = (cur.sp.w[j / 2] >> (16 * (j & 1))) & 0xFFFFu;
+            prv[j] = (cur.pr.w[j / 4] >> (8 * (j & 3))) & 0xFFu;
+        }
+#if PG_PROBE_STREAM
+        for (int j = 0; j < P; j++) o[j] = sv[j] ^ dv[j] ^ dpv[j] ^ prv[j] ^ spv[j];
+#else
+        if constexpr (NODE) classify_node_q<MODE, COUNT, P, STAGE && PG_PRED>(T, T.node, img, sv, dv, spv, dpv, prv, h, o, hook);
+        else classify_q<MODE, COUNT, P, STAGE && PG_PRED>(T, blobs, tab0, sv, dv, spv, dpv, prv, h, o);
+#endif
+        Words<P> ow;
+#pragma unroll
+        for (int j = 0; j < P; j++) ow.w[j] = o[j];
+        st_words<P>(ow, out + q * P);
         cur = nxt;
         q = qn;
     }
     // remainder (or everything when the pointers are not vector-aligned): one tuple per lane
-    for (uint64_t i = (nfull << 2) + first; i < n; i += stride) {
+    for (uint64_t i = nfull * P + first; i < n; i += stride) {
         const uint32_t s1[1] = {src[i]}, d1[1] = {dst[i]}, sp1[1] = {MODE == 2 ? (uint32_t)sport[i] : 0u},
                        dp1[1] = {dport[i]}, pr1[1] = {proto[i]};
         uint32_t o[1];
-        if constexpr (NODE) classify_node_q<MODE, COUNT, 1>(T, T.node, img, s1, d1, sp1, dp1, pr1, h, o);
-        else classify_q<MODE, COUNT, 1>(T, blobs, tab0, s1, d1, sp1, dp1, pr1, h, o);
+        if constexpr (NODE) classify_node_q<MODE, COUNT, 1, STAGE && PG_PRED>(T, T.node, img, s1, d1, sp1, dp1, pr1, h, o);
+        else classify_q<MODE, COUNT, 1, STAGE && PG_PRED>(T, blobs, tab0, s1, d1, sp1, dp1, pr1, h, o);
         out[i] = o[0];
     }
     if (COUNT && use_lds) {
         __syncthreads();
-        for (uint32_t i = threadIdx.x; i < T.n_slots; i += kBlock) {
+        for (uint32_t i = threadIdx.x; i < T.n_slots; i += BS) {
             const uint32_t v = hist[i];
             if (v) atomicAdd(&counters[i], (unsigned long long)v);
         }
@@ -391,12 +457,17 @@ static uint32_t g_blocks_per_cu = 0;        // 0: as many workgroups per CU as f
 static uint32_t g_stage_max_words = 16384;  // blobs up to 64 KiB are staged in LDS
 static uint32_t g_node_stage_max_words = 16384;  // node images up to 64 KiB are staged in LDS
 static uint32_t g_node_path = 1;            // PERPOD / CONN through the node classifier when built
+// workgroup size of LDS-staged classify launches; 0 = per mode (SINGLE / PERPOD 512, CONN 256:
+// tools/sweep.py on MI355X; CONN's register footprint wants the finer occupancy steps)
+static uint32_t g_block_stage = 0;
 
 int dev_set_tuning(const std::string& key, int value) {
     if (key == "blocks_per_cu" && value >= 0 && value <= 64) g_blocks_per_cu = (uint32_t)value;
     else if (key == "stage_max_words" && value >= 0 && value <= 36864) g_stage_max_words = (uint32_t)value;
     else if (key == "node_stage_max_words" && value >= 0 && value <= 36864) g_node_stage_max_words = (uint32_t)value;
     else if (key == "node_path" && (value == 0 || value == 1)) g_node_path = (uint32_t)value;
+    else if (key == "block_stage" && (value == 0 || value == 256 || value == 512 || value == 1024))
+        g_block_stage = (uint32_t)value;
     else return -1;
     return 0;
 }
@@ -423,23 +494,42 @@ static int grid_for(uint64_t items) {
 // (registers / LDS of this instantiation), so no workgroup waits for another to finish, capped
 // by the work and by blocks_per_cu when set.
 template <class K>
-static int grid_resident(K kernel, size_t lds, uint64_t items) {
+static int grid_resident(K kernel, int bs, size_t lds, uint64_t items) {
     int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kBlock, lds) != hipSuccess || per_cu < 1)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, bs, lds) != hipSuccess || per_cu < 1)
         per_cu = 1;
     if (g_blocks_per_cu) per_cu = std::min<int>(per_cu, (int)g_blocks_per_cu);
-    const uint64_t g = (items + kBlock - 1) / kBlock;
+    const uint64_t g = (items + bs - 1) / bs;
     return (int)std::max<uint64_t>(1, std::min<uint64_t>(g, (uint64_t)num_cus() * per_cu));
 }
 
+template <int MODE, bool COUNT, bool VEC, bool STAGE, bool NODE, int BS>
+static void launch_bs(const DevTableSet& T, int t, const uint32_t* src, const uint32_t* dst, const uint16_t* sport,
+                      const uint16_t* dport, const uint8_t* proto, uint64_t n, uint32_t* out,
+                      unsigned long long* counters, hipStream_t st, size_t hist, uint32_t stage, uint64_t items) {
+    auto k = k_classify<MODE, COUNT, VEC, STAGE, NODE, BS>;
+    const size_t lds = hist + (size_t)stage * 4;
+    hipLaunchKernelGGL(k, dim3(grid_resident(k, BS, lds, items)), dim3(BS), lds, st, T, t, src, dst, sport, dport,
+                       proto, n, out, counters, stage);
+}
+
+// Workgroup size: a staged image is shared by the workgroup, so larger workgroups hold more
+// waves per CU for the same LDS.
 template <int MODE, bool COUNT, bool VEC, bool STAGE, bool NODE>
 static void launch_one(const DevTableSet& T, int t, const uint32_t* src, const uint32_t* dst, const uint16_t* sport,
                        const uint16_t* dport, const uint8_t* proto, uint64_t n, uint32_t* out,
                        unsigned long long* counters, hipStream_t st, size_t hist, uint32_t stage, uint64_t items) {
-    auto k = k_classify<MODE, COUNT, VEC, STAGE, NODE>;
-    const size_t lds = hist + (size_t)stage * 4;
-    hipLaunchKernelGGL(k, dim3(grid_resident(k, lds, items)), dim3(kBlock), lds, st, T, t, src, dst, sport, dport,
-                       proto, n, out, counters, stage);
+    if constexpr (STAGE) {
+        const uint32_t bs = g_block_stage ? g_block_stage : (MODE == 2 ? 256u : 512u);
+        if (bs == 1024u)
+            return launch_bs<MODE, COUNT, VEC, STAGE, NODE, 1024>(T, t, src, dst, sport, dport, proto, n, out, counters,
+                                                                  st, hist, stage, items);
+        if (bs == 512u)
+            return launch_bs<MODE, COUNT, VEC, STAGE, NODE, 512>(T, t, src, dst, sport, dport, proto, n, out, counters,
+                                                                 st, hist, stage, items);
+    }
+    launch_bs<MODE, COUNT, VEC, STAGE, NODE, 256>(T, t, src, dst, sport, dport, proto, n, out, counters, st, hist, stage,
+                                                  items);
 }
 
 template <int MODE, bool COUNT, bool VEC>
@@ -447,7 +537,7 @@ static void launch_classify(const DevTableSet& T, int t, const uint32_t* src, co
                             const uint16_t* sport, const uint16_t* dport, const uint8_t* proto, uint64_t n,
                             uint32_t* out, unsigned long long* counters, hipStream_t st) {
     const size_t hist = (COUNT && T.n_slots <= kLdsHistMax) ? T.n_slots * 4 : 0;
-    const uint64_t items = VEC ? (n + 3) / 4 : n;
+    const uint64_t items = VEC ? (n + PG_TPL - 1) / PG_TPL : n;
     if constexpr (MODE == 0) {
         const DevTable& hd = T.host_tabs[t];
         const uint32_t words = T.host_blob_words[t];
@@ -488,8 +578,10 @@ int dev_classify(const DevTableSet& T, int mode, int table_id, const uint32_t* s
                  unsigned long long* counters, void* stream, std::string* err) {
     if (n == 0) return 0;
     auto al = [](const void* p, uintptr_t a) { return ((uintptr_t)p & (a - 1)) == 0; };
-    const bool vec = al(src, 16) && al(dst, 16) && al(dport, 8) && al(proto, 4) && al(out, 16) &&
-                     (mode != 2 || al(sport, 8));
+    // the group loads: 4*P-byte src/dst/out (16-B pieces), 2*P-byte ports, P-byte protocols
+    constexpr uintptr_t kPort = 2 * PG_TPL > 16 ? 16 : 2 * PG_TPL, kProto = PG_TPL > 16 ? 16 : PG_TPL;
+    const bool vec = al(src, 16) && al(dst, 16) && al(dport, kPort) && al(proto, kProto) && al(out, 16) &&
+                     (mode != 2 || al(sport, kPort));
     hipStream_t st = (hipStream_t)stream;
     const bool count = counters != nullptr;
     if (mode == 0) dispatch_mode<0>(count, vec, T, table_id, src, dst, sport, dport, proto, n, out, counters, st);

@@ -253,7 +253,8 @@ class Engine:
         self._ck(lib.pg_debug_walk_blob(self.h, _b(acl_name), p(a[0]), p(a[1]), p(a[2]), p(a[3]), n, p(out)))
         return out
 
-    def debug_classify_host(self, mode, table_id, src, dst, sport, dport, proto, counters=False, node=True):
+    def debug_classify_host(self, mode, table_id, src, dst, sport, dport, proto, counters=False, node=True,
+                            pred=True):
         """TESTS ONLY: pg_classify's per-tuple code run on the host (pg_debug_classify_host).
         -> verdict words (u32), and the u64 hit counters when ``counters``."""
         import numpy as np
@@ -265,7 +266,8 @@ class Engine:
         out = np.empty(n, np.uint32)
         cnt = np.zeros(self.num_counter_slots(), np.uint64) if counters else None
         self._ck(lib.pg_debug_classify_host(self.h, mode, table_id, C.byref(t), n, p(out),
-                                            p(cnt) if counters else None, int(node)))
+                                            p(cnt) if counters else None,
+                                            int(node) | (2 if pred else 0)))
         return (out, cnt) if counters else out
 
     def node_stats(self):
