@@ -154,8 +154,28 @@ struct Hist {
     unsigned long long* glob;
     PG_HD void inc(uint32_t slot) const {
 #if defined(__HIP_DEVICE_COMPILE__)
-        if (lds) atomicAdd(&lds[slot], 1u);
-        else if (glob) atomicAdd(&glob[slot], 1ull);
+        // A few slots take most hits (a reflective ACL's rule, "no ACL", a default deny):
+        // twice, the lanes sharing the first active lane's slot add their count with one
+        // atomic; the rest add one each.
+        bool done = false;
+#pragma unroll
+        for (int r = 0; r < 2; r++) {
+            if (!done) {
+                const uint32_t lead = __builtin_amdgcn_readfirstlane(slot);
+                const unsigned long long m = __ballot(slot == lead);
+                if (slot == lead) {
+                    if (__lane_id() == (unsigned)(__ffsll((long long)m) - 1)) {
+                        if (lds) atomicAdd(&lds[lead], (uint32_t)__popcll(m));
+                        else if (glob) atomicAdd(&glob[lead], (unsigned long long)__popcll(m));
+                    }
+                    done = true;
+                }
+            }
+        }
+        if (!done) {
+            if (lds) atomicAdd(&lds[slot], 1u);
+            else if (glob) atomicAdd(&glob[slot], 1ull);
+        }
 #else
         if (glob) glob[slot]++;
 #endif
