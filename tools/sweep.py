@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--tune", action="append", default=[], help="key=v1,v2,...")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--counters", action="store_true", help="classify with per-rule hit counters")
     a = ap.parse_args()
     kw = {"n_tuples": a.tuples} if a.tuples else {}
     w = W.CONFIGS[a.config](0, **kw)
@@ -43,6 +44,8 @@ def main():
     combos = list(itertools.product(*vals)) if keys else [()]
     lib = _capi.lib
     outs = [torch.empty(n, dtype=torch.int32, device="cuda") for _ in combos]
+    cnt = torch.zeros(e.num_counter_slots(), dtype=torch.int64, device="cuda") if a.counters else None
+    cptr = cnt.data_ptr() if a.counters else None
     soa = b.soa()
     stream = C.c_void_p(torch.cuda.current_stream().cuda_stream)
     times = {i: [] for i in range(len(combos))}
@@ -51,10 +54,10 @@ def main():
             for k, v in zip(keys, combo):
                 assert lib.pg_set_tuning(k.encode(), v) == 0, (k, v)
             ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            lib.pg_classify(e.h, w.mode, w.table_id, C.byref(soa), n, outs[i].data_ptr(), None, stream)  # warm
+            lib.pg_classify(e.h, w.mode, w.table_id, C.byref(soa), n, outs[i].data_ptr(), cptr, stream)  # warm
             ev0.record()
             for _ in range(a.reps):
-                assert lib.pg_classify(e.h, w.mode, w.table_id, C.byref(soa), n, outs[i].data_ptr(), None,
+                assert lib.pg_classify(e.h, w.mode, w.table_id, C.byref(soa), n, outs[i].data_ptr(), cptr,
                                        stream) == 0
             ev1.record()
             torch.cuda.synchronize()
@@ -64,7 +67,7 @@ def main():
     name = os.path.basename(os.environ.get("VPP_AMD_LIB", "libpolicygpu.so"))
     for i, combo in enumerate(combos):
         ms = float(np.median(times[i]))
-        print(json.dumps({"lib": name, "config": a.config, **dict(zip(keys, combo)), "ms": round(ms, 4),
+        print(json.dumps({"lib": name, "config": a.config, "counters": a.counters, **dict(zip(keys, combo)), "ms": round(ms, 4),
                           "gpps": round(n / ms / 1e6, 1), "GBps": round(n * bpt / ms / 1e6, 1),
                           "same_output": bool(torch.equal(outs[i], ref))}), flush=True)
 

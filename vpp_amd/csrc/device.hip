@@ -189,6 +189,16 @@ __device__ __forceinline__ void stream_store(V v, V* p) {
 #ifndef PG_PRED  // predicated (branch-free) trie walks on LDS-staged images (A/B: slower)
 #define PG_PRED 0
 #endif
+// tuples of a group classified together (lockstep chunk), per mode, each dividing PG_TPL
+#ifndef PG_QSINGLE
+#define PG_QSINGLE 4
+#endif
+#ifndef PG_QPOD
+#define PG_QPOD 4
+#endif
+#ifndef PG_QCONN
+#define PG_QCONN 1
+#endif
 #ifndef PG_TPL  // tuples per lane per loop iteration (4 or 8)
 #define PG_TPL 4
 #endif
@@ -303,8 +313,26 @@ __global__ __launch_bounds__(BS) void k_classify(DevTableSet T, int32_t t, const
 #if PG_PROBE_STREAM
         for (int j = 0; j < P; j++) o[j] = sv[j] ^ dv[j] ^ dpv[j] ^ prv[j] ^ spv[j];
 #else
-        if constexpr (NODE) classify_node_q<MODE, COUNT, P, STAGE && PG_PRED>(T, T.node, img, sv, dv, spv, dpv, prv, h, o, hook);
-        else classify_q<MODE, COUNT, P, STAGE && PG_PRED>(T, blobs, tab0, sv, dv, spv, dpv, prv, h, o);
+        // per-mode chunk: the group's P tuples are classified QC at a time (less state per
+        // lane, more waves per SIMD)
+        constexpr int QC = MODE == 2 ? PG_QCONN : (MODE == 1 ? PG_QPOD : PG_QSINGLE);
+#pragma unroll
+        for (int c = 0; c < P; c += QC) {
+            uint32_t cs[QC], cd[QC], csp[QC], cdp[QC], cpr[QC], co[QC];
+#pragma unroll
+            for (int j = 0; j < QC; j++)
+                cs[j] = sv[c + j], cd[j] = dv[c + j], csp[j] = spv[c + j], cdp[j] = dpv[c + j], cpr[j] = prv[c + j];
+            if constexpr (NODE) {
+                if (c == 0)
+                    classify_node_q<MODE, COUNT, QC, STAGE && PG_PRED>(T, T.node, img, cs, cd, csp, cdp, cpr, h, co, hook);
+                else
+                    classify_node_q<MODE, COUNT, QC, STAGE && PG_PRED>(T, T.node, img, cs, cd, csp, cdp, cpr, h, co);
+            } else {
+                classify_q<MODE, COUNT, QC, STAGE && PG_PRED>(T, blobs, tab0, cs, cd, csp, cdp, cpr, h, co);
+            }
+#pragma unroll
+            for (int j = 0; j < QC; j++) o[c + j] = co[j];
+        }
 #endif
         Words<P> ow;
 #pragma unroll
@@ -457,8 +485,8 @@ static uint32_t g_blocks_per_cu = 0;        // 0: as many workgroups per CU as f
 static uint32_t g_stage_max_words = 16384;  // blobs up to 64 KiB are staged in LDS
 static uint32_t g_node_stage_max_words = 16384;  // node images up to 64 KiB are staged in LDS
 static uint32_t g_node_path = 1;            // PERPOD / CONN through the node classifier when built
-// workgroup size of LDS-staged classify launches; 0 = per mode (SINGLE / PERPOD 512, CONN 256:
-// tools/sweep.py on MI355X; CONN's register footprint wants the finer occupancy steps)
+// workgroup size of LDS-staged classify launches; 0 = per mode (SINGLE 1024, PERPOD / CONN
+// 512: tools/sweep.py on MI355X)
 static uint32_t g_block_stage = 0;
 
 int dev_set_tuning(const std::string& key, int value) {
@@ -520,7 +548,7 @@ static void launch_one(const DevTableSet& T, int t, const uint32_t* src, const u
                        const uint16_t* dport, const uint8_t* proto, uint64_t n, uint32_t* out,
                        unsigned long long* counters, hipStream_t st, size_t hist, uint32_t stage, uint64_t items) {
     if constexpr (STAGE) {
-        const uint32_t bs = g_block_stage ? g_block_stage : (MODE == 2 ? 256u : 512u);
+        const uint32_t bs = g_block_stage ? g_block_stage : (MODE == 0 ? 1024u : 512u);
         if (bs == 1024u)
             return launch_bs<MODE, COUNT, VEC, STAGE, NODE, 1024>(T, t, src, dst, sport, dport, proto, n, out, counters,
                                                                   st, hist, stage, items);
