@@ -23,6 +23,9 @@ constexpr uint32_t kFlagCross = 1u, kFlagLists = 2u, kFlagCand = 4u, kFlagLinear
 constexpr uint32_t kLeaf = 0x80000000u;
 constexpr uint32_t kSrcRoot = 16u;       // the src trie root follows the 16-word blob header
 constexpr uint32_t kWalkKeyLimit = 0x30000u;  // keys >= this (ANY protocol) take the linear path
+// key bound of records that match every key: covers the whole 18-bit walk range, ANY keys
+// included, so every list terminates for any key the walk is given
+constexpr uint32_t kRecKeyAll = 0x3FFFFu;
 
 struct W2 {
     uint32_t x, y;
@@ -48,8 +51,9 @@ PG_HD bool rec_match(const W4& r, uint32_t dst, uint32_t key) {
     return (dst & rec_mask((r.y >> 18) & 63u)) == r.x && key >= (r.y & 0x3FFFFu) && key <= r.z;
 }
 
-// on[j]: tuple j is walked (table present, not LINEAR, key < kWalkKeyLimit). w[j] is only
-// written for those.
+// on[j]: tuple j is walked (table present, not LINEAR). w[j] is only written for those. Keys
+// must be < 2^18; the result for keys >= kWalkKeyLimit (ANY protocol) is meaningless and the
+// caller replaces it.
 // PRED: the trie descent issues a load for every tuple at every level (a finished tuple
 // re-reads word 0) instead of branching per tuple: cheaper when the blob is in LDS, where a
 // wasted read costs little and per-lane branches cost exec-mask juggling.

@@ -25,8 +25,10 @@ namespace pg {
 #define PG_NOINLINE inline
 #endif
 
+// TCP -> port, UDP -> 0x10000 | port, OTHER -> 0x20000, anything else -> 0x30000 (branch-free)
 PG_HD uint32_t pkt_key(uint32_t proto, uint32_t port) {
-    return proto == 0u ? port : (proto == 1u ? (kKeyUDP | port) : (proto == 2u ? kKeyOTHER : kKeyANY));
+    const uint32_t p = proto < 3u ? proto : 3u;
+    return (p << 16) | (p < 2u ? port : 0u);
 }
 PG_HD uint32_t verdict(uint32_t act, uint32_t slot) { return (act << 30) | slot; }
 constexpr uint32_t kSlotMask = 0x3FFFFFFFu;
@@ -94,16 +96,19 @@ PG_HD void eval_q(const DevTableSet& T, const uint32_t* blobs, const DevTable (&
     DevLoader ld[Q];
     BlobTab tb[Q];
     bool on[Q];
+    // on[j] depends on the table only (uniform when every lane has the same table, as in
+    // SINGLE mode); ANY-protocol keys (< 2^18, a valid trie address) are walked too and their
+    // result replaced by the linear scan below
     PG_UNROLL
     for (int j = 0; j < Q; j++) {
         ld[j] = DevLoader{blobs + tab[j].blob_off};
         tb[j] = BlobTab{tab[j].fsk, tab[j].dflt, tab[j].kroot, tab[j].xoff, tab[j].nkc};
-        on[j] = act[j] && !(tab[j].fsk & kFlagLinear) && key[j] < kWalkKeyLimit;
+        on[j] = act[j] && !(tab[j].fsk & kFlagLinear);
     }
     blob_walk<PRED>(ld, tb, on, src, dst, key, w);
     PG_UNROLL
     for (int j = 0; j < Q; j++)
-        if (act[j] && !on[j])
+        if (act[j] && (!on[j] || key[j] >= kWalkKeyLimit))
             w[j] = eval_linear(T.rules, tab[j].rule_base, tab[j].n_rules, tab[j].dflt, src[j], dst[j], key[j]);
 }
 

@@ -331,9 +331,9 @@ bool build_fast_table(const DevRule* rules, uint32_t n, uint32_t rule_base, uint
             for (uint32_t r : L) {
                 uint32_t l = 0;
                 dlen(rules[r].dmask, &l);
-                put_rec(rules[r].dnet, l, 0, kKeyMax, verdict(r));  // key already covered by the class
+                put_rec(rules[r].dnet, l, 0, kRecKeyAll, verdict(r));  // key already covered by the class
             }
-            put_rec(0, 0, 0, kKeyMax, cverd[e]);  // fall through to the pair's verdict
+            put_rec(0, 0, 0, kRecKeyAll, cverd[e]);  // fall through to the pair's verdict
         }
         return true;
     }
@@ -361,7 +361,7 @@ bool build_fast_table(const DevRule* rules, uint32_t n, uint32_t rule_base, uint
             dlen(rules[r].dmask, &l);
             put_rec(rules[r].dnet, l, rules[r].klo, rules[r].khi, verdict(r));
         }
-        put_rec(0, 0, 0, kKeyMax, dflt);  // no candidate matched: the table's default deny
+        put_rec(0, 0, 0, kRecKeyAll, dflt);  // no candidate matched: the table's default deny
     }
     return true;
 }
@@ -509,12 +509,12 @@ bool build_node(HostTableSet& h, const std::vector<TableAnalysis*>& an, const st
                         const DevRule& R = A.rules[r];
                         recs.push_back(R.dnet);
                         recs.push_back((uint32_t)__builtin_popcount(R.dmask) << 18);
-                        recs.push_back(kKeyMax);
+                        recs.push_back(kRecKeyAll);
                         recs.push_back(((R.act & 3u) << 30) | (A.rule_base + r));
                     }
                     recs.push_back(0);
                     recs.push_back(0);
-                    recs.push_back(kKeyMax);
+                    recs.push_back(kRecKeyAll);
                     recs.push_back(A.cverd[e]);
                 }
                 X.push_back(kNodeList | first[e]);
