@@ -37,8 +37,8 @@ MODE_NAME = {0: "single", 1: "perpod", 2: "conn"}
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=20)
-    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--steps", type=int, default=200)
+    p.add_argument("--warmup", type=int, default=50)
     p.add_argument("--config", type=int, default=2, choices=sorted(W.CONFIGS))
     p.add_argument("--tuples", type=int, default=0, help="tuples per GPU (default: the config's)")
     p.add_argument("--counters", action="store_true", help="time with per-rule hit counters on")
