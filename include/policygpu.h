@@ -264,6 +264,87 @@ typedef struct pg_conn_query {
 /* out[i] = ConnAction; out_slot (optional) = deciding slot per query */
 int pg_connections(pg_ctx* ctx, const pg_conn_query* q, size_t n, int32_t* out, uint32_t* out_slot);
 
+/* ---- policy configurator ------------------------------------------
+ * configurator.PolicyConfiguratorAPI / Txn (plugins/policy/configurator/configurator_api.go:28-54,
+ * configurator_impl.go:104-472): K8s-shaped policies per pod -> ordered ContivRule lists
+ * rendered into every registered renderer (the GPU ACL renderer and/or mock renderers).
+ * The policy cache's pod data (LookupPod) and the IPAM NAT-loopback address are set
+ * explicitly. Go nil-vs-empty matters for Match.Pods / IPBlocks: *_nil = 1 means nil. */
+enum { PG_POLICY_INGRESS = 0, PG_POLICY_EGRESS = 1, PG_POLICY_ALL = 2 }; /* configurator.PolicyType */
+enum { PG_MATCH_INGRESS = 0, PG_MATCH_EGRESS = 1 };                       /* configurator.MatchType  */
+enum { PG_PORT_TCP = 0, PG_PORT_UDP = 1 };                                /* configurator.ProtocolType */
+typedef struct pg_pod_id {
+    const char* ns;
+    const char* name;
+} pg_pod_id;
+typedef struct pg_cfg_port { /* configurator.Port */
+    int32_t protocol;
+    uint16_t number;
+    uint16_t _pad;
+} pg_cfg_port;
+typedef struct pg_ipblock { /* configurator.IPBlock */
+    pg_ipnet network;
+    const pg_ipnet* except;
+    size_t n_except;
+} pg_ipblock;
+typedef struct pg_match { /* configurator.Match */
+    int32_t type;
+    int32_t pods_nil;
+    const pg_pod_id* pods;
+    size_t n_pods;
+    int32_t blocks_nil;
+    int32_t _pad;
+    const pg_ipblock* blocks;
+    size_t n_blocks;
+    const pg_cfg_port* ports;
+    size_t n_ports;
+} pg_match;
+typedef struct pg_policy { /* configurator.ContivPolicy */
+    pg_pod_id id;
+    int32_t type;
+    int32_t _pad;
+    const pg_match* matches;
+    size_t n_matches;
+} pg_policy;
+
+typedef struct pg_configurator pg_configurator;
+typedef struct pg_cfg_txn pg_cfg_txn;
+typedef struct pg_mock_renderer pg_mock_renderer;
+
+pg_configurator* pg_configurator_new(void);
+void pg_configurator_free(pg_configurator* c);
+const char* pg_configurator_last_error(const pg_configurator* c);
+/* PolicyConfigurator.RegisterRenderer (configurator_impl.go:104-107); the renderer must
+ * outlive the configurator's transactions */
+int pg_configurator_register_renderer(pg_configurator* c, pg_renderer* r);
+int pg_configurator_register_mock(pg_configurator* c, pg_mock_renderer* r);
+/* policy cache LookupPod data: ip = NULL removes the pod, "" = known without an address */
+int pg_configurator_set_pod(pg_configurator* c, const char* ns, const char* name, const char* ip);
+/* IPAM.NatLoopbackIP() (net.ParseIP form; NULL or unparsable = nil) */
+int pg_configurator_set_nat_loopback(pg_configurator* c, const char* ip);
+pg_cfg_txn* pg_configurator_new_txn(pg_configurator* c, int resync);
+/* Txn.Configure: replaces the pod's set of policies (copied) */
+int pg_cfg_txn_configure(pg_cfg_txn* t, const char* ns, const char* name, const pg_policy* policies, size_t n);
+/* Txn.Commit: renders every configured pod into every renderer and commits them; frees t.
+ * PG_EFAULT (message in pg_configurator_last_error) when a renderer's Commit failed. */
+int pg_cfg_txn_commit(pg_cfg_txn* t);
+void pg_cfg_txn_free(pg_cfg_txn* t);
+
+/* mock/renderer.MockRenderer (mock/renderer/renderer_mock.go:39-185): stores the rendered
+ * lists; TestTraffic evaluates them. direction: 0 = INGRESS (from the pod
+ * to the vswitch), 1 = EGRESS; result: 0 DENIED, 1 ALLOWED, 2 UNMATCHED. */
+pg_mock_renderer* pg_mock_renderer_new(void);
+void pg_mock_renderer_free(pg_mock_renderer* r);
+/* GetPodIP: writes the address ("" when unknown) and the mask length */
+int pg_mock_renderer_pod_ip(pg_mock_renderer* r, const char* ns, const char* name, char* ip, size_t cap,
+                            int* masklen);
+/* the pod's ingress/egress list in rendered order -> number of rules (PG_ENOENT: no pod) */
+int pg_mock_renderer_rules(pg_mock_renderer* r, const char* ns, const char* name, int direction,
+                           pg_contiv_rule* out, size_t cap);
+int pg_mock_renderer_test_traffic(pg_mock_renderer* r, const char* ns, const char* name, int direction,
+                                  const char* src_ip, const char* dst_ip, int protocol, uint16_t src_port,
+                                  uint16_t dst_port);
+
 #ifdef __cplusplus
 }
 #endif

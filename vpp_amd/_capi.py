@@ -76,6 +76,29 @@ class pg_conn_query(C.Structure):
                 ("dst_ip", C.c_char_p), ("protocol", C.c_int32), ("src_port", C.c_uint16), ("dst_port", C.c_uint16)]
 
 
+class pg_pod_id(C.Structure):
+    _fields_ = [("ns", C.c_char_p), ("name", C.c_char_p)]
+
+
+class pg_cfg_port(C.Structure):
+    _fields_ = [("protocol", C.c_int32), ("number", C.c_uint16), ("_pad", C.c_uint16)]
+
+
+class pg_ipblock(C.Structure):
+    _fields_ = [("network", pg_ipnet), ("except_", C.POINTER(pg_ipnet)), ("n_except", C.c_size_t)]
+
+
+class pg_match(C.Structure):
+    _fields_ = [("type", C.c_int32), ("pods_nil", C.c_int32), ("pods", C.POINTER(pg_pod_id)), ("n_pods", C.c_size_t),
+                ("blocks_nil", C.c_int32), ("_pad", C.c_int32), ("blocks", C.POINTER(pg_ipblock)),
+                ("n_blocks", C.c_size_t), ("ports", C.POINTER(pg_cfg_port)), ("n_ports", C.c_size_t)]
+
+
+class pg_policy(C.Structure):
+    _fields_ = [("id", pg_pod_id), ("type", C.c_int32), ("_pad", C.c_int32), ("matches", C.POINTER(pg_match)),
+                ("n_matches", C.c_size_t)]
+
+
 _P = C.c_void_p
 _SIGS = {
     "pg_version": (C.c_char_p, []),
@@ -117,6 +140,24 @@ _SIGS = {
                                          C.c_int]),
     "pg_node_stats": (C.c_int, [_P, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.POINTER(C.c_uint64),
                                 C.POINTER(C.c_uint64)]),
+    "pg_configurator_new": (_P, []),
+    "pg_configurator_free": (None, [_P]),
+    "pg_configurator_last_error": (C.c_char_p, [_P]),
+    "pg_configurator_register_renderer": (C.c_int, [_P, _P]),
+    "pg_configurator_register_mock": (C.c_int, [_P, _P]),
+    "pg_configurator_set_pod": (C.c_int, [_P, C.c_char_p, C.c_char_p, C.c_char_p]),
+    "pg_configurator_set_nat_loopback": (C.c_int, [_P, C.c_char_p]),
+    "pg_configurator_new_txn": (_P, [_P, C.c_int]),
+    "pg_cfg_txn_configure": (C.c_int, [_P, C.c_char_p, C.c_char_p, C.POINTER(pg_policy), C.c_size_t]),
+    "pg_cfg_txn_commit": (C.c_int, [_P]),
+    "pg_cfg_txn_free": (None, [_P]),
+    "pg_mock_renderer_new": (_P, []),
+    "pg_mock_renderer_free": (None, [_P]),
+    "pg_mock_renderer_pod_ip": (C.c_int, [_P, C.c_char_p, C.c_char_p, C.c_char_p, C.c_size_t, C.POINTER(C.c_int)]),
+    "pg_mock_renderer_rules": (C.c_int, [_P, C.c_char_p, C.c_char_p, C.c_int, C.POINTER(pg_contiv_rule),
+                                         C.c_size_t]),
+    "pg_mock_renderer_test_traffic": (C.c_int, [_P, C.c_char_p, C.c_char_p, C.c_int, C.c_char_p, C.c_char_p, C.c_int,
+                                                C.c_uint16, C.c_uint16]),
     "pg_classify_linear": (C.c_int, [_P, C.c_int, C.POINTER(pg_tuple_soa), C.c_uint64, _P, _P]),
     "pg_counters_device": (_P, [_P]),
     "pg_reset_counters": (C.c_int, [_P, _P]),

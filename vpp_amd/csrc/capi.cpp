@@ -4,27 +4,12 @@
 #include <memory>
 #include <stdexcept>
 
-#include "../../include/policygpu.h"
+#include "capi_internal.hpp"
 #include "classify.hpp"
-#include "engine.hpp"
 
 using namespace pg;
 
-struct pg_ctx {
-    Engine eng;
-};
-struct pg_renderer {
-    pg_ctx* ctx;
-    std::unique_ptr<Renderer> r;
-};
-struct pg_txn {
-    pg_ctx* ctx;
-    std::unique_ptr<RendererTxn> t;
-};
-
-namespace {
-
-IPNet to_ipnet(const pg_ipnet& n) {
+IPNet pg::to_ipnet(const pg_ipnet& n) {
     IPNet r;
     if (n.family == 4) {
         r.ip = mk(n.addr, 4);
@@ -35,6 +20,26 @@ IPNet to_ipnet(const pg_ipnet& n) {
     }
     return r;
 }
+
+pg_ipnet pg::to_pg_ipnet(const IPNet& n) {
+    pg_ipnet v{};
+    if (n.ip.len == 0) return v;
+    int ones = 0, bits = 0;
+    mask_size(n.mask, &ones, &bits);
+    Bytes v4;
+    if (to4(n.ip, &v4) && bits == 32) {
+        v.family = 4;
+        std::memcpy(v.addr, v4.b, 4);
+    } else {
+        v.family = 6;
+        const Bytes b16 = to16(n.ip);
+        std::memcpy(v.addr, b16.b, 16);
+    }
+    v.prefix_len = (uint8_t)(ones < 0 ? 0 : ones);
+    return v;
+}
+
+namespace {
 
 ContivRule to_rule(const pg_contiv_rule& c) {
     ContivRule r;
