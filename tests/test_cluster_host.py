@@ -99,3 +99,59 @@ def test_world_connections_equal_python_oracle(cluster):
         assert act[i] == a1[0]
         exp_slot = (e.slot_of_rule(e.table_id(names[t]), int(i1[0])) if t >= 0 else e.num_counter_slots() - 2)
         assert slot[i] == exp_slot
+
+
+def test_cluster_via_configurator_equals_oracle_chain():
+    """Configs 3/5 are built by the policy configurator from K8s-shaped policies
+    (workloads.cluster_engine): at a reduced size, the ACLs it installs equal those of the
+    oracle configurator feeding the oracle ACL renderer."""
+    from oracle import configurator as OC
+    from oracle import gonet
+    pods = W.cluster_pods(N_NS, PODS, APPS)
+    pols = W.cluster_policies(pods, N_NS, APPS)
+    # product chain: the workload builder itself, at this size
+    e = R.Engine(0)
+    e.SetMainInterfaceName("GbE")
+    e.SetVxlanBVIIfName("VXLAN-BVI")
+    e.SetHostInterconnectIfName("VPP-Host")
+    import vpp_amd.workloads as WW
+    orig = WW._new_engine
+    WW._new_engine = lambda device: e
+    try:
+        e2, _, local, _ = W.cluster_engine(0, N_NS, PODS, APPS)
+    finally:
+        WW._new_engine = orig
+    assert e2 is e
+    # oracle chain
+    as_dict = lambda p: {  # noqa: E731
+        "id": "%s/%s" % p.ID, "type": p.Type,
+        "matches": [{"type": m.Type, "pods": None if m.Pods is None else ["%s/%s" % R._pod(x) for x in m.Pods],
+                     "blocks": None if m.IPBlocks is None else [
+                         {"network": repr(b.Network), "except": [repr(x) for x in b.Except]} for b in m.IPBlocks],
+                     "ports": [{"protocol": x.Protocol, "number": x.Number} for x in m.Ports]} for m in p.Matches]}
+    ocfg = OC.PolicyConfigurator({p["id"]: W.ip_str(p["ip"]) for p in pods}, W.NAT_LOOPBACK_IP)
+    mock = OC.MockRenderer()
+    ocfg.renderers.append(mock)
+    t = ocfg.new_txn(True)
+    for p in pods:
+        if not p["remote"]:
+            t.configure(p["id"], [as_dict(x) for x in pols[(p["ns"], p["app"])]])
+    t.commit()
+    pod_ifs = {p["id"]: "tap-%s" % p["id"].replace("/", "-") for p in pods if not p["remote"]}
+    setup = {"pod_ifs": pod_ifs, "host_interconnect": "VPP-Host", "main_if": "GbE", "other_ifs": [],
+             "vxlan_bvi": "VXLAN-BVI", "pods": [(p["id"], W.ip_str(p["ip"]), p["remote"]) for p in pods]}
+    ora = kd.OracleBackend()
+    ora.setup(setup)
+
+    def d(r):
+        net = lambda n: "" if n.is_empty() else gonet.ipnet_string(n)  # noqa: E731
+        return {"action": "PERMIT" if r.action else "DENY", "src": net(r.src), "dst": net(r.dst),
+                "proto": {0: "TCP", 1: "UDP", 2: "OTHER", 3: "ANY"}[r.protocol], "sport": r.src_port,
+                "dport": r.dst_port}
+    renders = [{"pod": p, "ip": gonet.ip_string(c[0].ip), "ingress": [d(r) for r in c[1]],
+                "egress": [d(r) for r in c[2]], "removed": False} for p, c in sorted(mock.config.items())]
+    assert ora.txn(True, renders) is None
+    o, p = oracle_acls(ora.engine), product_acls(e)
+    assert sorted(o) == sorted(p) and len(o) > 3
+    for name in o:
+        assert o[name] == p[name], name

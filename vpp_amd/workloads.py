@@ -7,8 +7,8 @@ this path); shapes follow the reference's own fixtures and perf generator:
   config 2  1k-rule single table shaped like tests/policy/perf/gen-policy.py (/16-/24 CIDRs
             under (i+0x100)<<16 minus five /24-/32 excepts, x 20 TCP/UDP ports), first 999
             generated rules + deny-the-rest, 64M tuples (bench.py's default)
-  config 3  1k pods / 10 namespaces / per-app policies -> local tables + global table,
-            per-pod (egress interface) mode
+  config 3  1k pods / 10 namespaces / per-app K8s policies -> policy configurator -> ACL
+            renderer: local tables + global table, per-pod (egress interface) mode
   config 4  100k-rule ACL ingested directly (vpp_acl key space), disjoint src prefixes,
             first-match depth Zipf(1.1), 5 % no-match
   config 5  config-3 topology in connection mode with per-rule hit counters
@@ -266,7 +266,47 @@ def cluster_rules(pods, n_ns, apps):
     return ingress, egress
 
 
+def cluster_policies(pods, n_ns, apps):
+    """The K8s policies behind cluster_rules, as configurator.ContivPolicy objects: one per
+    (namespace, app), selecting the peer pods by label (expanded to pod IDs, as the policy
+    processor does), IPBlocks with excepts, ports. The configurator turns them into the
+    ContivRule lists (adding the NAT-loopback permit and the deny-the-rest rules)."""
+    from . import configurator as CF
+    by = {}
+    for p in pods:
+        by.setdefault((p["ns"], p["app"]), []).append(p["id"])
+    out = {}
+    for k in range(n_ns):
+        for a in range(apps):
+            ingress = [  # traffic to the pod (the vswitch's egress direction)
+                CF.Match(CF.MatchIngress, Pods=by[(k, (a + 1) % apps)],
+                         Ports=[CF.Port(CF.TCP, 80), CF.Port(CF.TCP, 8080)]),
+                CF.Match(CF.MatchIngress, Pods=by[((k + 1) % n_ns, a)], Ports=[CF.Port(CF.TCP, 443)]),
+                CF.Match(CF.MatchIngress, Pods=[q for kk in ((k + 3) % n_ns, (k + 5) % n_ns, (k + 7) % n_ns)
+                                                for q in by[(kk, (a + 2) % apps)]],
+                         Ports=[CF.Port(CF.UDP, 53), CF.Port(CF.UDP, 5353)]),
+                CF.Match(CF.MatchIngress, IPBlocks=[CF.IPBlock("192.168.0.0/16", ["192.168.10.0/24"])],
+                         Ports=[CF.Port(CF.TCP, 22)]),
+            ]
+            pols = [CF.ContivPolicy("ns%d/app%d-ingress" % (k, a), CF.PolicyIngress, ingress)]
+            if a == 0:  # app-0 pods also restrict what they send
+                pols.append(CF.ContivPolicy("ns%d/app%d-egress" % (k, a), CF.PolicyEgress, [
+                    CF.Match(CF.MatchEgress, Ports=[CF.Port(CF.TCP, 443)]),
+                    CF.Match(CF.MatchEgress, IPBlocks=[CF.IPBlock("10.96.0.10/32")], Ports=[CF.Port(CF.UDP, 53)]),
+                    CF.Match(CF.MatchEgress, IPBlocks=[CF.IPBlock("10.1.%d.0/24" % k)],
+                             Ports=[CF.Port(CF.TCP, 80)]),
+                ]))
+            out[(k, a)] = pols
+    return out
+
+
+NAT_LOOPBACK_IP = "10.1.255.254"
+
+
 def cluster_engine(device=0, n_ns=10, pods_per_ns=100, apps=5):
+    """Configs 3/5: the cluster's policies -> policy configurator (every pod in its cache, the
+    pods of this node configured) -> GPU ACL renderer -> engine."""
+    from . import configurator as CF
     e = _new_engine(device)
     pods = cluster_pods(n_ns, pods_per_ns, apps)
     local = {}
@@ -276,13 +316,17 @@ def cluster_engine(device=0, n_ns=10, pods_per_ns=100, apps=5):
             e.SetPodIfName(p["id"], ifn)
             local[p["ip"]] = ifn
         e.RegisterPod(p["id"], ip_str(p["ip"]), p["remote"])
-    ingress, egress = cluster_rules(pods, n_ns, apps)
+    policies = cluster_policies(pods, n_ns, apps)
     r = R.Renderer(e)
-    t = r.NewTxn(True)
+    cfg = CF.PolicyConfigurator()
     for p in pods:
-        if not p["remote"]:  # the renderer is told about the pods of this node
-            key = (p["ns"], p["app"])
-            t.Render(p["id"], R.IPNet.host(ip_str(p["ip"])), ingress[key], egress[key], False)
+        cfg.AddPodConfig(p["id"], ip_str(p["ip"]))
+    cfg.SetNatLoopbackIP(NAT_LOOPBACK_IP)
+    assert cfg.RegisterRenderer(r) is None
+    t = cfg.NewTxn(True)
+    for p in pods:
+        if not p["remote"]:  # the configurator of this node is told about its own pods
+            t.Configure(p["id"], policies[(p["ns"], p["app"])])
     err = t.Commit()
     assert err is None, err
     pool = [p["ip"] for p in pods] + [ip_u32(x) for x in INTERNET_HOSTS] * 10
