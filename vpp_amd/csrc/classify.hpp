@@ -302,7 +302,11 @@ struct NodeEval {
         for (int j = 0; j < Q; j++) {
             pend[j] = false;
             if (!on[j]) continue;
+#if defined(PG_PROBE_NOGATHER)  // measurement build only: no cross-entry load
+            w[j] = pos[j] & 0x3FFFu;
+#else
             w[j] = X.u32(pos[j]);
+#endif
         }
         if (!*hooked) {
             *hooked = true;
@@ -512,7 +516,12 @@ PG_HD void classify_node_q(const DevTableSet& T, const DevNode& N, const L& img,
     uint32_t ips[2 * Q], ipc[2 * Q];
     PG_UNROLL
     for (int j = 0; j < Q; j++) ips[j] = s[j], ips[Q + j] = d[j];
+#if defined(PG_PROBE_NOWALK)  // measurement build only: IP classes without the trie walk
+    PG_UNROLL
+    for (int j = 0; j < 2 * Q; j++) ipc[j] = ips[j] % N.n_ipc;
+#else
     node_trie_q<PRED>(img, 0u, N.ip_s1, 32u, ips, ipc);
+#endif
     uint32_t cs[Q], cd[Q], gs[Q], ga[Q];
     if (MODE == 2) {
         uint32_t keys[2 * Q], kc[2 * Q];
