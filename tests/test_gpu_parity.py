@@ -319,3 +319,32 @@ def test_node_kernel_equals_per_table_kernel(config):
     assert np.array_equal(c1, c2) and np.array_equal(c1, c3)
     host = e.debug_classify_host(w.mode, -1, *b.numpy(b.n), node=True)
     assert np.array_equal(host, staged)
+
+
+def test_large_table_root_staged_and_hbm_walks_equal_oracle():
+    """A table whose blob exceeds LDS (candidate mode, level-compressed tries): the launch
+    that stages only the src-trie root (STAGE 2) and the one that reads everything from HBM
+    both equal evalACL."""
+    rnd = random.Random(42)
+    rules = []
+    for k in range(20000):
+        rules.append({"action": k % 2, "src": "10.%d.%d.%d/%d" % (k // 4096, (k // 16) % 256, (k % 16) * 16,
+                                                                    rnd.choice([28, 29, 30, 31, 32])), "dst": "",
+                      "udp": {"src": [0, 65535], "dst": [k % 1000, k % 1000 + 5]}})
+    rules += fz.rand_acl(rnd, 50, fz.ANCHORS, weird=True, tail="deny")
+    e = make_engine({"big": (None, rules)})
+    tid = e.table_id("out-big")
+    assert e.table_stats(tid)["structure"] == "cand" and e.table_stats(tid)["blob_bytes"] > (64 << 10)
+    anchors = [(10 << 24) | (k << 4) for k in range(0, 20000, 13)] + fz.ANCHORS
+    tup = fz.rand_tuples(np.random.default_rng(42), 200003, anchors, any_pct=0.02)
+    ea, es = expected_single(e, tid, rules, tup)
+    outs = []
+    for root_words in (16400, 0):
+        assert R.lib.pg_set_tuning(b"stage_root_max_words", root_words) == 0
+        try:
+            got, _ = run_single(e, tid, tup)
+        finally:
+            R.lib.pg_set_tuning(b"stage_root_max_words", 16400)
+        assert ((got >> 30) == ea).all() and ((got & 0x3FFFFFFF) == es).all()
+        outs.append(got)
+    assert np.array_equal(outs[0], outs[1])

@@ -1,4 +1,5 @@
 set -o pipefail
-for L in libpolicygpu.so libpolicygpu_nogather.so libpolicygpu_nowalk.so libpolicygpu_nowalknogather.so libpolicygpu_probe0.so; do
-  VPP_AMD_LIB=vpp_amd/$L timeout -k 10 200 python tools/sweep.py --config 3 --rounds 3 --reps 10 || exit 1
+for r in 1 2; do
+  VPP_AMD_LIB=vpp_amd/libpolicygpu_old.so timeout -k 10 200 python tools/sweep.py --config 4 --rounds 3 --reps 10 || exit 1
+  VPP_AMD_LIB=vpp_amd/libpolicygpu.so timeout -k 10 200 python tools/sweep.py --config 4 --tune stage_root_max_words=16400,0 --rounds 3 --reps 10 || exit 1
 done

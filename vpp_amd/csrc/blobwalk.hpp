@@ -21,6 +21,10 @@ namespace pg {
 
 constexpr uint32_t kFlagCross = 1u, kFlagLists = 2u, kFlagCand = 4u, kFlagLinear = 8u;
 constexpr uint32_t kLeaf = 0x80000000u;
+// non-leaf trie entry: child block offset (words) | child stride << kTrieStrideShift
+constexpr uint32_t kTrieStrideShift = 26u, kTrieChildMask = (1u << kTrieStrideShift) - 1u;
+PG_HD uint32_t trie_child(uint32_t e) { return e & kTrieChildMask; }
+PG_HD uint32_t trie_stride(uint32_t e) { return (e >> kTrieStrideShift) & 31u; }
 constexpr uint32_t kSrcRoot = 16u;       // the src trie root follows the 16-word blob header
 constexpr uint32_t kWalkKeyLimit = 0x30000u;  // keys >= this (ANY protocol) take the linear path
 // key bound of records that match every key: covers the whole 18-bit walk range, ANY keys
@@ -57,9 +61,11 @@ PG_HD bool rec_match(const W4& r, uint32_t dst, uint32_t key) {
 // PRED: the trie descent issues a load for every tuple at every level (a finished tuple
 // re-reads word 0) instead of branching per tuple: cheaper when the blob is in LDS, where a
 // wasted read costs little and per-lane branches cost exec-mask juggling.
-template <bool PRED = false, class L, int Q>
-PG_HD void blob_walk(const L (&ld)[Q], const BlobTab (&tb)[Q], const bool (&on)[Q], const uint32_t (&src)[Q],
-                     const uint32_t (&dst)[Q], const uint32_t (&key)[Q], uint32_t (&w)[Q]) {
+// ld0: loaders for the src trie root (a blob whose root alone is staged in LDS: ld0 reads the
+// LDS copy, ld the blob in HBM; otherwise the same loaders).
+template <bool PRED = false, class L, class L0, int Q>
+PG_HD void blob_walk(const L (&ld)[Q], const L0 (&ld0)[Q], const BlobTab (&tb)[Q], const bool (&on)[Q],
+                     const uint32_t (&src)[Q], const uint32_t (&dst)[Q], const uint32_t (&key)[Q], uint32_t (&w)[Q]) {
     uint32_t es[Q], ek[Q], ss[Q], sk[Q];
     PG_UNROLL
     for (int j = 0; j < Q; j++) {
@@ -67,7 +73,7 @@ PG_HD void blob_walk(const L (&ld)[Q], const BlobTab (&tb)[Q], const bool (&on)[
         ss[j] = sk[j] = 0;
         if (on[j]) {
             ss[j] = 32u - ((tb[j].fsk >> 8) & 0xFFu);
-            es[j] = ld[j].u32(kSrcRoot + (src[j] >> ss[j]));
+            es[j] = ld0[j].u32(kSrcRoot + (src[j] >> ss[j]));
             if (tb[j].fsk & kFlagCross) {
                 sk[j] = 18u - (tb[j].fsk >> 16);
                 ek[j] = ld[j].u32(tb[j].kroot + (key[j] >> sk[j]));
@@ -84,10 +90,10 @@ PG_HD void blob_walk(const L (&ld)[Q], const BlobTab (&tb)[Q], const bool (&on)[
         for (int j = 0; j < Q; j++) {
             if (PRED) {
                 const bool ds = !(es[j] & kLeaf), dk = !(ek[j] & kLeaf);
-                const uint32_t ts = ss[j] < 8u ? ss[j] : 8u, tk = sk[j] < 8u ? sk[j] : 8u;
+                const uint32_t ts = ds ? trie_stride(es[j]) : 0u, tk = dk ? trie_stride(ek[j]) : 0u;
                 const uint32_t ns = ss[j] - ts, nk = sk[j] - tk;
-                const uint32_t is = ds ? es[j] + ((src[j] >> ns) & ((1u << ts) - 1u)) : 0u;
-                const uint32_t ik = dk ? ek[j] + ((key[j] >> nk) & ((1u << tk) - 1u)) : 0u;
+                const uint32_t is = ds ? trie_child(es[j]) + ((src[j] >> ns) & ((1u << ts) - 1u)) : 0u;
+                const uint32_t ik = dk ? trie_child(ek[j]) + ((key[j] >> nk) & ((1u << tk) - 1u)) : 0u;
                 const uint32_t vs = ld[j].u32(is), vk = ld[j].u32(ik);
                 es[j] = ds ? vs : es[j];
                 ek[j] = dk ? vk : ek[j];
@@ -96,14 +102,14 @@ PG_HD void blob_walk(const L (&ld)[Q], const BlobTab (&tb)[Q], const bool (&on)[
                 continue;
             }
             if (!(es[j] & kLeaf)) {
-                const uint32_t st = ss[j] < 8u ? ss[j] : 8u;
+                const uint32_t st = trie_stride(es[j]);
                 ss[j] -= st;
-                es[j] = ld[j].u32(es[j] + ((src[j] >> ss[j]) & ((1u << st) - 1u)));
+                es[j] = ld[j].u32(trie_child(es[j]) + ((src[j] >> ss[j]) & ((1u << st) - 1u)));
             }
             if (!(ek[j] & kLeaf)) {
-                const uint32_t st = sk[j] < 8u ? sk[j] : 8u;
+                const uint32_t st = trie_stride(ek[j]);
                 sk[j] -= st;
-                ek[j] = ld[j].u32(ek[j] + ((key[j] >> sk[j]) & ((1u << st) - 1u)));
+                ek[j] = ld[j].u32(trie_child(ek[j]) + ((key[j] >> sk[j]) & ((1u << st) - 1u)));
             }
         }
     }
@@ -149,6 +155,12 @@ PG_HD void blob_walk(const L (&ld)[Q], const BlobTab (&tb)[Q], const bool (&on)[
             }
         }
     }
+}
+
+template <bool PRED = false, class L, int Q>
+PG_HD void blob_walk(const L (&ld)[Q], const BlobTab (&tb)[Q], const bool (&on)[Q], const uint32_t (&src)[Q],
+                     const uint32_t (&dst)[Q], const uint32_t (&key)[Q], uint32_t (&w)[Q]) {
+    blob_walk<PRED>(ld, ld, tb, on, src, dst, key, w);
 }
 
 struct HostLoader {

@@ -90,10 +90,13 @@ PG_HD DevTable load_tab(const DevTable* tabs, int32_t t) {
 // evalACL of Q tuples against their tables' per-table blobs, in lockstep.
 // act[j]: evaluate tuple j against tab[j]; blobs: base the tables' blob_off is relative to
 // (the global blob array, or the LDS copy of a staged table).
+// rootb (SINGLE mode, a blob whose src-trie root alone is staged): the LDS copy of the
+// table blob's first words, read for the root load only.
 template <bool PRED = false, int Q>
 PG_HD void eval_q(const DevTableSet& T, const uint32_t* blobs, const DevTable (&tab)[Q], const bool (&act)[Q],
-                  const uint32_t (&src)[Q], const uint32_t (&dst)[Q], const uint32_t (&key)[Q], uint32_t (&w)[Q]) {
-    DevLoader ld[Q];
+                  const uint32_t (&src)[Q], const uint32_t (&dst)[Q], const uint32_t (&key)[Q], uint32_t (&w)[Q],
+                  const uint32_t* rootb = nullptr) {
+    DevLoader ld[Q], ld0[Q];
     BlobTab tb[Q];
     bool on[Q];
     // on[j] depends on the table only (uniform when every lane has the same table, as in
@@ -102,10 +105,11 @@ PG_HD void eval_q(const DevTableSet& T, const uint32_t* blobs, const DevTable (&
     PG_UNROLL
     for (int j = 0; j < Q; j++) {
         ld[j] = DevLoader{blobs + tab[j].blob_off};
+        ld0[j] = rootb ? DevLoader{rootb} : ld[j];
         tb[j] = BlobTab{tab[j].fsk, tab[j].dflt, tab[j].kroot, tab[j].xoff, tab[j].nkc};
         on[j] = act[j] && !(tab[j].fsk & kFlagLinear);
     }
-    blob_walk<PRED>(ld, tb, on, src, dst, key, w);
+    blob_walk<PRED>(ld, ld0, tb, on, src, dst, key, w);
     PG_UNROLL
     for (int j = 0; j < Q; j++)
         if (act[j] && (!on[j] || key[j] >= kWalkKeyLimit))
@@ -211,7 +215,7 @@ struct TabEval {
 // table per evaluation, cross[tabinfo[t].base + ipclass * nkc_t + kmap[t][keyclass]]: a
 // verdict, or (kNodeList) the first of the dst records to test. Tables the node does not
 // cover, LINEAR tables and ANY-protocol packets take the per-table path.
-// Q trie lookups in lockstep (root stride s1 over a W-bit address, then 8-bit strides).
+// Q trie lookups in lockstep (root stride s1 over a W-bit address, then each node's stride).
 // PRED: one load per tuple per level, no per-tuple branches (LDS images).
 template <bool PRED, class L, int Q>
 PG_HD void node_trie_q(const L& ld, uint32_t root, uint32_t s1, uint32_t W, const uint32_t (&a)[Q], uint32_t (&c)[Q]) {
@@ -230,16 +234,16 @@ PG_HD void node_trie_q(const L& ld, uint32_t root, uint32_t s1, uint32_t W, cons
         for (int j = 0; j < Q; j++) {
             if (PRED) {
                 const bool d = !(e[j] & kLeaf);
-                const uint32_t st = sh[j] < 8u ? sh[j] : 8u, ns = sh[j] - st;
-                const uint32_t v = ld.u32(d ? e[j] + ((a[j] >> ns) & ((1u << st) - 1u)) : 0u);
+                const uint32_t st = d ? trie_stride(e[j]) : 0u, ns = sh[j] - st;
+                const uint32_t v = ld.u32(d ? trie_child(e[j]) + ((a[j] >> ns) & ((1u << st) - 1u)) : 0u);
                 e[j] = d ? v : e[j];
                 sh[j] = d ? ns : sh[j];
                 continue;
             }
             if (e[j] & kLeaf) continue;
-            const uint32_t st = sh[j] < 8u ? sh[j] : 8u;
+            const uint32_t st = trie_stride(e[j]);
             sh[j] -= st;
-            e[j] = ld.u32(e[j] + ((a[j] >> sh[j]) & ((1u << st) - 1u)));
+            e[j] = ld.u32(trie_child(e[j]) + ((a[j] >> sh[j]) & ((1u << st) - 1u)));
         }
     }
     PG_UNROLL
@@ -458,7 +462,7 @@ PG_HD void conn_q(const DevTableSet& T, const EV& ev, const End (&es)[Q], const 
 template <int MODE, bool COUNT, int Q, bool PRED = false>
 PG_HD void classify_q(const DevTableSet& T, const uint32_t* blobs, const DevTable& tab0, const uint32_t (&s)[Q],
                       const uint32_t (&d)[Q], const uint32_t (&sp)[Q], const uint32_t (&dp)[Q],
-                      const uint32_t (&pr)[Q], const Hist& h, uint32_t (&out)[Q]) {
+                      const uint32_t (&pr)[Q], const Hist& h, uint32_t (&out)[Q], const uint32_t* rootb = nullptr) {
     uint32_t key[Q], kack[Q];
     PG_UNROLL
     for (int j = 0; j < Q; j++) key[j] = pkt_key(pr[j], dp[j]), kack[j] = pkt_key(pr[j], sp[j]);
@@ -467,7 +471,7 @@ PG_HD void classify_q(const DevTableSet& T, const uint32_t* blobs, const DevTabl
         bool act[Q];
         PG_UNROLL
         for (int j = 0; j < Q; j++) tab[j] = tab0, act[j] = true;
-        eval_q<PRED>(T, blobs, tab, act, s, d, key, out);
+        eval_q<PRED>(T, blobs, tab, act, s, d, key, out, rootb);
         if (COUNT) {
             PG_UNROLL
             for (int j = 0; j < Q; j++) h.inc(out[j] & kSlotMask);

@@ -171,8 +171,10 @@ __device__ __forceinline__ void stream_store(V v, V* p) {
     else *p = v;
 }
 
-// STAGE (SINGLE mode only): the table's blob (stage_words u32, multiple of 4) is copied into
-// LDS once per workgroup and every lookup of the grid-stride loop reads it from there.
+// STAGE (SINGLE mode): 1 = the table's blob (stage_words u32, multiple of 4) is copied into
+// LDS once per workgroup and every lookup of the grid-stride loop reads it from there; 2 = a
+// blob too large for LDS has its header and src-trie root (stage_words) copied, so the first
+// dependent load of every lookup hits LDS and the rest read HBM / L2.
 // NODE (PERPOD / CONN): the node classifier; STAGE then copies the node image into LDS.
 //
 // Stream pipelining (PG_PREFETCH): 1 = the next group's loads are issued at the top of each
@@ -231,7 +233,7 @@ __device__ __forceinline__ void st_words(const Words<NW>& v, uint32_t* p) {
     for (int k = 0; k < NW / 4; k++)
         stream_store(v4u{v.w[4 * k], v.w[4 * k + 1], v.w[4 * k + 2], v.w[4 * k + 3]}, reinterpret_cast<v4u*>(p) + k);
 }
-template <int MODE, bool COUNT, bool VEC, bool STAGE, bool NODE, int BS>
+template <int MODE, bool COUNT, bool VEC, int STAGE, bool NODE, int BS>
 __global__ __launch_bounds__(BS) void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
                                                      const uint32_t* __restrict__ dst,
                                                      const uint16_t* __restrict__ sport,
@@ -256,10 +258,14 @@ __global__ __launch_bounds__(BS) void k_classify(DevTableSet T, int32_t t, const
         if (STAGE) {
             const uint4* g = reinterpret_cast<const uint4*>(T.blobs + tab0.blob_off);
             for (uint32_t i = threadIdx.x; i < stage_words / 4u; i += BS) reinterpret_cast<uint4*>(smem)[i] = g[i];
-            blobs = smem;
-            tab0.blob_off = 0;
+            if (STAGE == 1) {
+                blobs = smem;
+                tab0.blob_off = 0;
+            }
         }
     }
+    // STAGE 2: only the header and src-trie root of a large blob are in LDS
+    const uint32_t* rootb = (MODE == 0 && STAGE == 2) ? smem : nullptr;
     if (COUNT && use_lds) {
         for (uint32_t i = threadIdx.x; i < T.n_slots; i += BS) hist[i] = 0;
         h.lds = hist;
@@ -328,7 +334,7 @@ __global__ __launch_bounds__(BS) void k_classify(DevTableSet T, int32_t t, const
                 else
                     classify_node_q<MODE, COUNT, QC, STAGE && PG_PRED>(T, T.node, img, cs, cd, csp, cdp, cpr, h, co);
             } else {
-                classify_q<MODE, COUNT, QC, STAGE && PG_PRED>(T, blobs, tab0, cs, cd, csp, cdp, cpr, h, co);
+                classify_q<MODE, COUNT, QC, STAGE == 1 && PG_PRED>(T, blobs, tab0, cs, cd, csp, cdp, cpr, h, co, rootb);
             }
 #pragma unroll
             for (int j = 0; j < QC; j++) o[c + j] = co[j];
@@ -347,7 +353,7 @@ __global__ __launch_bounds__(BS) void k_classify(DevTableSet T, int32_t t, const
                        dp1[1] = {dport[i]}, pr1[1] = {proto[i]};
         uint32_t o[1];
         if constexpr (NODE) classify_node_q<MODE, COUNT, 1, STAGE && PG_PRED>(T, T.node, img, s1, d1, sp1, dp1, pr1, h, o);
-        else classify_q<MODE, COUNT, 1, STAGE && PG_PRED>(T, blobs, tab0, s1, d1, sp1, dp1, pr1, h, o);
+        else classify_q<MODE, COUNT, 1, STAGE == 1 && PG_PRED>(T, blobs, tab0, s1, d1, sp1, dp1, pr1, h, o, rootb);
         out[i] = o[0];
     }
     if (COUNT && use_lds) {
@@ -482,8 +488,9 @@ __global__ void k_conn_queries(DevTableSet T, const ConnQueryDev* q, uint32_t n,
 
 // ---- launchers --------------------------------------------------------------------------------
 static uint32_t g_blocks_per_cu = 0;        // 0: as many workgroups per CU as fit (occupancy)
-static uint32_t g_stage_max_words = 16384;  // blobs up to 64 KiB are staged in LDS
+static uint32_t g_stage_max_words = kStageBlobWords;  // blobs up to 64 KiB are staged in LDS
 static uint32_t g_node_stage_max_words = 16384;  // node images up to 64 KiB are staged in LDS
+static uint32_t g_stage_root_max_words = 16400;  // larger blobs: header + src root up to 2^14 entries
 static uint32_t g_node_path = 1;            // PERPOD / CONN through the node classifier when built
 // workgroup size of LDS-staged classify launches; 0 = per mode (SINGLE 1024, PERPOD / CONN
 // 512: tools/sweep.py on MI355X)
@@ -493,6 +500,7 @@ int dev_set_tuning(const std::string& key, int value) {
     if (key == "blocks_per_cu" && value >= 0 && value <= 64) g_blocks_per_cu = (uint32_t)value;
     else if (key == "stage_max_words" && value >= 0 && value <= 36864) g_stage_max_words = (uint32_t)value;
     else if (key == "node_stage_max_words" && value >= 0 && value <= 36864) g_node_stage_max_words = (uint32_t)value;
+    else if (key == "stage_root_max_words" && value >= 0 && value <= 36864) g_stage_root_max_words = (uint32_t)value;
     else if (key == "node_path" && (value == 0 || value == 1)) g_node_path = (uint32_t)value;
     else if (key == "block_stage" && (value == 0 || value == 256 || value == 512 || value == 1024))
         g_block_stage = (uint32_t)value;
@@ -531,7 +539,7 @@ static int grid_resident(K kernel, int bs, size_t lds, uint64_t items) {
     return (int)std::max<uint64_t>(1, std::min<uint64_t>(g, (uint64_t)num_cus() * per_cu));
 }
 
-template <int MODE, bool COUNT, bool VEC, bool STAGE, bool NODE, int BS>
+template <int MODE, bool COUNT, bool VEC, int STAGE, bool NODE, int BS>
 static void launch_bs(const DevTableSet& T, int t, const uint32_t* src, const uint32_t* dst, const uint16_t* sport,
                       const uint16_t* dport, const uint8_t* proto, uint64_t n, uint32_t* out,
                       unsigned long long* counters, hipStream_t st, size_t hist, uint32_t stage, uint64_t items) {
@@ -543,7 +551,7 @@ static void launch_bs(const DevTableSet& T, int t, const uint32_t* src, const ui
 
 // Workgroup size: a staged image is shared by the workgroup, so larger workgroups hold more
 // waves per CU for the same LDS.
-template <int MODE, bool COUNT, bool VEC, bool STAGE, bool NODE>
+template <int MODE, bool COUNT, bool VEC, int STAGE, bool NODE>
 static void launch_one(const DevTableSet& T, int t, const uint32_t* src, const uint32_t* dst, const uint16_t* sport,
                        const uint16_t* dport, const uint8_t* proto, uint64_t n, uint32_t* out,
                        unsigned long long* counters, hipStream_t st, size_t hist, uint32_t stage, uint64_t items) {
@@ -569,22 +577,26 @@ static void launch_classify(const DevTableSet& T, int t, const uint32_t* src, co
     if constexpr (MODE == 0) {
         const DevTable& hd = T.host_tabs[t];
         const uint32_t words = T.host_blob_words[t];
+        const uint32_t root_words = (kSrcRoot + (1u << ((hd.fsk >> 8) & 0xFFu)) + 3u) & ~3u;
         if (!(hd.fsk & kFlagLinear) && words && words <= g_stage_max_words)
-            launch_one<MODE, COUNT, VEC, true, false>(T, t, src, dst, sport, dport, proto, n, out, counters, st, hist,
-                                                      words, items);
+            launch_one<MODE, COUNT, VEC, 1, false>(T, t, src, dst, sport, dport, proto, n, out, counters, st, hist,
+                                                   words, items);
+        else if (!(hd.fsk & kFlagLinear) && words && root_words <= g_stage_root_max_words)
+            launch_one<MODE, COUNT, VEC, 2, false>(T, t, src, dst, sport, dport, proto, n, out, counters, st, hist,
+                                                   root_words, items);
         else
-            launch_one<MODE, COUNT, VEC, false, false>(T, t, src, dst, sport, dport, proto, n, out, counters, st,
-                                                       hist, 0, items);
+            launch_one<MODE, COUNT, VEC, 0, false>(T, t, src, dst, sport, dport, proto, n, out, counters, st, hist,
+                                                   0, items);
     } else if (g_node_path && T.node.img) {
         if (T.node.img_words <= g_node_stage_max_words)
-            launch_one<MODE, COUNT, VEC, true, true>(T, t, src, dst, sport, dport, proto, n, out, counters, st, hist,
-                                                     T.node.img_words, items);
+            launch_one<MODE, COUNT, VEC, 1, true>(T, t, src, dst, sport, dport, proto, n, out, counters, st, hist,
+                                                  T.node.img_words, items);
         else
-            launch_one<MODE, COUNT, VEC, false, true>(T, t, src, dst, sport, dport, proto, n, out, counters, st, hist,
-                                                      0, items);
+            launch_one<MODE, COUNT, VEC, 0, true>(T, t, src, dst, sport, dport, proto, n, out, counters, st, hist,
+                                                  0, items);
     } else {
-        launch_one<MODE, COUNT, VEC, false, false>(T, t, src, dst, sport, dport, proto, n, out, counters, st, hist, 0,
-                                                   items);
+        launch_one<MODE, COUNT, VEC, 0, false>(T, t, src, dst, sport, dport, proto, n, out, counters, st, hist, 0,
+                                               items);
     }
 }
 

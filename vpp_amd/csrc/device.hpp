@@ -96,8 +96,13 @@ struct HostTableSet {
 // fastpath.cpp: classification blob of one table (false = does not fit the budgets). When
 // `an` is given it receives the table's class analysis for build_node.
 struct TableAnalysis;
+// table blobs up to this many words are staged in LDS by default (64 KiB); larger ones are
+// read from HBM and compiled with level-compressed tries
+constexpr uint32_t kStageBlobWords = 16384;
+// lc: level-compressed tries (wider strides in dense subtrees) for blobs read from HBM
 bool build_fast_table(const DevRule* rules, uint32_t n, uint32_t rule_base, uint32_t default_slot,
-                      std::vector<uint32_t>& blob, uint64_t cross_budget, TableAnalysis** an = nullptr);
+                      std::vector<uint32_t>& blob, uint64_t cross_budget, TableAnalysis** an = nullptr,
+                      bool lc = false);
 void free_analysis(TableAnalysis* an);
 // fastpath.cpp: the node classifier over the tables with an analysis (null = not covered).
 // pods: {IPv4, interface, inbound table, outbound table} of local pods; node_end: the same for

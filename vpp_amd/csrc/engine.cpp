@@ -208,8 +208,15 @@ void Engine::compile() {
         DevTable& hdr = h.tabs[t];
         std::vector<uint32_t> blob;
         hdr.dflt = (kActDeny << 30) | (NR + (uint32_t)t);
-        if (build_fast_table(h.rules.data() + hdr.rule_base, hdr.n_rules, hdr.rule_base, NR + (uint32_t)t, blob,
-                             1ull << 22, &an[t])) {
+        bool ok = build_fast_table(h.rules.data() + hdr.rule_base, hdr.n_rules, hdr.rule_base, NR + (uint32_t)t, blob,
+                                   1ull << 22, &an[t]);
+        if (ok && blob.size() > kStageBlobWords) {  // read from HBM: one dependent load fewer in dense subtrees
+            std::vector<uint32_t> lc;
+            if (build_fast_table(h.rules.data() + hdr.rule_base, hdr.n_rules, hdr.rule_base, NR + (uint32_t)t, lc,
+                                 1ull << 22, nullptr, true))
+                blob.swap(lc);
+        }
+        if (ok) {
             while (blob.size() % 4) blob.push_back(0);
             hdr.blob_off = (uint32_t)h.blobs.size();
             hdr.fsk = blob[0] | (blob[3] << 8) | (blob[5] << 16);

@@ -57,9 +57,16 @@ struct VecHash {
 };
 
 // Multibit trie over [0, 2^W): intervals given by sorted starts `bnd` (bnd[0] == 0) and a
-// class per interval. Appends blocks to `blob`; returns the root offset.
+// class per interval. Appends blocks to `blob`; returns the root offset, or kTrieFail when
+// the blob outgrows the 2^26-word child pointers. A non-leaf entry holds its child's offset
+// and stride (blobwalk.hpp trie_child/trie_stride); children take 8-bit strides, or with
+// `lc` (level compression, for tries read from HBM) 18 / 16 / 12 bits when their span holds
+// at least 8192 / 2048 / 256 interval boundaries: about the memory of the 8-bit levels they
+// replace, one or two dependent loads fewer.
+constexpr uint32_t kTrieFail = 0xFFFFFFFFu;
+constexpr uint32_t kLcRootBits = 14;  // HBM-resident blobs: the root alone is staged in LDS (64 KiB)
 uint32_t build_trie(std::vector<uint32_t>& blob, const std::vector<uint64_t>& bnd, const std::vector<uint32_t>& cls,
-                    uint32_t W, uint32_t s1) {
+                    uint32_t W, uint32_t s1, bool lc = false) {
     // interval index containing address a
     auto find = [&](uint64_t a) { return (size_t)(std::upper_bound(bnd.begin(), bnd.end(), a) - bnd.begin()) - 1; };
     struct Job {
@@ -89,9 +96,16 @@ uint32_t build_trie(std::vector<uint32_t>& blob, const std::vector<uint64_t>& bn
                 continue;
             }
             uint32_t st = std::min<uint32_t>(8, j.shift);
+            if (lc && j.shift >= 12) {
+                const size_t inside = (size_t)(std::lower_bound(bnd.begin(), bnd.end(), a + span) - bnd.begin()) - k - 1;
+                if (j.shift >= 18 && inside >= 8192) st = 18;
+                else if (j.shift >= 16 && inside >= 2048) st = 16;
+                else if (inside >= 256) st = 12;
+            }
             uint32_t child = (uint32_t)blob.size();
+            if ((uint64_t)child + (1ull << st) > kTrieChildMask) return kTrieFail;
             blob.resize(blob.size() + (1u << st), 0);
-            blob[j.block + e] = child;
+            blob[j.block + e] = child | (st << kTrieStrideShift);
             stack.push_back({child, a, j.shift - st, st});
         }
     }
@@ -140,7 +154,7 @@ void set_node_tuning(uint32_t enable, uint32_t root_bits) {
 }
 
 bool build_fast_table(const DevRule* rules, uint32_t n, uint32_t rule_base, uint32_t default_slot,
-                      std::vector<uint32_t>& blob, uint64_t cross_budget, TableAnalysis** an) {
+                      std::vector<uint32_t>& blob, uint64_t cross_budget, TableAnalysis** an, bool lc) {
     if (an) *an = nullptr;
     blob.assign(16, 0);
     const uint32_t dflt = (kActDeny << 30) | default_slot;
@@ -289,12 +303,13 @@ bool build_fast_table(const DevRule* rules, uint32_t n, uint32_t rule_base, uint
 
     if (cross) {
         const uint32_t nkc = (uint32_t)key_sets.size();
-        const uint32_t s1 = pick_stride(sb.size(), 32);
-        if (build_trie(blob, sb, sint_cls, 32, s1) != kSrcRoot) return false;
+        const uint32_t s1 = std::min<uint32_t>(pick_stride(sb.size(), 32), lc ? kLcRootBits : 32u);
+        if (build_trie(blob, sb, sint_cls, 32, s1, lc) != kSrcRoot) return false;
         blob[2] = kSrcRoot;
         blob[3] = s1;
         const uint32_t k1 = pick_stride(kb.size(), 18);
-        blob[4] = build_trie(blob, kb, kseg_cls, 18, k1);
+        blob[4] = build_trie(blob, kb, kseg_cls, 18, k1, lc);
+        if (blob[4] == kTrieFail) return false;
         blob[5] = k1;
         blob[7] = nkc;
         while (blob.size() % 4) blob.push_back(0);
@@ -348,8 +363,8 @@ bool build_fast_table(const DevRule* rules, uint32_t n, uint32_t rule_base, uint
     if (nrec >= (1ull << 29)) return false;
     std::vector<uint32_t> leaf(sb.size());
     for (size_t k = 0; k < sb.size(); k++) leaf[k] = first_rec[sint_cls[k]];
-    const uint32_t s1 = pick_stride(sb.size(), 32);
-    if (build_trie(blob, sb, leaf, 32, s1) != kSrcRoot) return false;
+    const uint32_t s1 = std::min<uint32_t>(pick_stride(sb.size(), 32), lc ? kLcRootBits : 32u);
+    if (build_trie(blob, sb, leaf, 32, s1, lc) != kSrcRoot) return false;
     blob[0] = kFlagCand;
     blob[2] = kSrcRoot;
     blob[3] = s1;
@@ -461,6 +476,7 @@ bool build_node(HostTableSet& h, const std::vector<TableAnalysis*>& an, const st
     if (build_trie(img, gb, gcls, 32, N.ip_s1) != 0) return false;
     N.key_k1 = std::min(pick_stride(kb.size(), 18), g_node_root_bits);
     N.key_root = build_trie(img, kb, kcls, 18, N.key_k1);
+    if (N.key_root == kTrieFail) return false;
     while (img.size() % 2) img.push_back(0);
     N.ipinfo = (uint32_t)img.size();
     for (uint32_t g = 0; g < G; g++) {
