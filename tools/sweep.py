@@ -30,8 +30,12 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--counters", action="store_true", help="classify with per-rule hit counters")
+    ap.add_argument("--pre", action="append", default=[], help="key=v set before the tables are compiled")
     a = ap.parse_args()
     kw = {"n_tuples": a.tuples} if a.tuples else {}
+    for t in a.pre:
+        k, v = t.split("=")
+        assert _capi.lib.pg_set_tuning(k.encode(), int(v)) == 0, t
     w = W.CONFIGS[a.config](0, **kw)
     e, n = w.engine, w.n_tuples
     b = D.TupleBatch(n, with_sport=(w.mode == 2))
@@ -67,7 +71,7 @@ def main():
     name = os.path.basename(os.environ.get("VPP_AMD_LIB", "libpolicygpu.so"))
     for i, combo in enumerate(combos):
         ms = float(np.median(times[i]))
-        print(json.dumps({"lib": name, "config": a.config, "counters": a.counters, **dict(zip(keys, combo)), "ms": round(ms, 4),
+        print(json.dumps({"lib": name, "config": a.config, "counters": a.counters, "pre": a.pre, **dict(zip(keys, combo)), "ms": round(ms, 4),
                           "gpps": round(n / ms / 1e6, 1), "GBps": round(n * bpt / ms / 1e6, 1),
                           "same_output": bool(torch.equal(outs[i], ref))}), flush=True)
 

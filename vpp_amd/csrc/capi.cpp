@@ -143,6 +143,12 @@ int pg_set_tuning(const char* key, int value) {
         set_root_bits_max((uint32_t)value);
         return PG_OK;
     }
+    if (std::string(key) == "lc_node" || std::string(key) == "lc_lds") {  // tables compiled afterwards
+        if (value != 0 && value != 1) return PG_EINVAL;
+        if (std::string(key) == "lc_node") set_lc_node((uint32_t)value);
+        else set_lc_lds((uint32_t)value);
+        return PG_OK;
+    }
     if (std::string(key) == "node_build" || std::string(key) == "node_root_bits") {  // tables compiled afterwards
         static uint32_t enable = 1, bits = 12;
         if (std::string(key) == "node_build") {

@@ -10,6 +10,9 @@
 
 namespace pg {
 
+uint32_t g_lc_lds = 0;
+void set_lc_lds(uint32_t on) { g_lc_lds = on; }
+
 // ---- compile one vpp_acl rule (aclengine_mock.go:510-649) --------------------------------
 // Every outcome of evalACL for a rule is expressed as (src predicate, dst predicate,
 // key range, action-on-key-match, action-for-ANY-packets):
@@ -210,10 +213,11 @@ void Engine::compile() {
         hdr.dflt = (kActDeny << 30) | (NR + (uint32_t)t);
         bool ok = build_fast_table(h.rules.data() + hdr.rule_base, hdr.n_rules, hdr.rule_base, NR + (uint32_t)t, blob,
                                    1ull << 22, &an[t]);
-        if (ok && blob.size() > kStageBlobWords) {  // read from HBM: one dependent load fewer in dense subtrees
+        if (ok && (blob.size() > kStageBlobWords || g_lc_lds)) {  // fewer dependent loads in dense subtrees
             std::vector<uint32_t> lc;
             if (build_fast_table(h.rules.data() + hdr.rule_base, hdr.n_rules, hdr.rule_base, NR + (uint32_t)t, lc,
-                                 1ull << 22, nullptr, true))
+                                 1ull << 22, nullptr, true) &&
+                (blob.size() > kStageBlobWords || lc.size() <= kStageBlobWords))
                 blob.swap(lc);
         }
         if (ok) {

@@ -126,6 +126,7 @@ bool unconditional(const DevRule& r) { return r.dmask == 0 && r.klo == 0 && r.kh
 bool live(const DevRule& r) { return r.klo <= r.khi; }  // can match a TCP/UDP/OTHER packet
 
 uint32_t g_node_enable = 1;
+uint32_t g_lc_node = 0;  // level-compressed node tries (LDS image)
 uint32_t g_node_root_bits = 12;           // node IPv4 trie root: 2^12 words = 16 KiB
 constexpr uint64_t kNodeCrossBudget = 1ull << 25;  // node cross entries (128 MiB)
 
@@ -148,6 +149,7 @@ struct TableAnalysis {
 void free_analysis(TableAnalysis* an) { delete an; }
 
 void set_root_bits_max(uint32_t bits) { g_root_bits_max = std::max<uint32_t>(4, std::min<uint32_t>(16, bits)); }
+void set_lc_node(uint32_t on) { g_lc_node = on; }
 void set_node_tuning(uint32_t enable, uint32_t root_bits) {
     g_node_enable = enable;
     g_node_root_bits = std::max<uint32_t>(4, std::min<uint32_t>(16, root_bits));
@@ -473,7 +475,7 @@ bool build_node(HostTableSet& h, const std::vector<TableAnalysis*>& an, const st
     std::vector<uint32_t>& img = h.node_img;
     DevNode& N = h.node;
     N.ip_s1 = std::min(pick_stride(gb.size(), 32), g_node_root_bits);
-    if (build_trie(img, gb, gcls, 32, N.ip_s1) != 0) return false;
+    if (build_trie(img, gb, gcls, 32, N.ip_s1, g_lc_node != 0) != 0) return false;
     N.key_k1 = std::min(pick_stride(kb.size(), 18), g_node_root_bits);
     N.key_root = build_trie(img, kb, kcls, 18, N.key_k1);
     if (N.key_root == kTrieFail) return false;
