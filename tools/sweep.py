@@ -31,8 +31,11 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--counters", action="store_true", help="classify with per-rule hit counters")
     ap.add_argument("--pre", action="append", default=[], help="key=v set before the tables are compiled")
+    ap.add_argument("--ns", type=int, default=0, help="configs 3/5: namespaces (default 10)")
     a = ap.parse_args()
     kw = {"n_tuples": a.tuples} if a.tuples else {}
+    if a.ns:
+        kw["n_ns"] = a.ns
     for t in a.pre:
         k, v = t.split("=")
         assert _capi.lib.pg_set_tuning(k.encode(), int(v)) == 0, t
@@ -71,7 +74,7 @@ def main():
     name = os.path.basename(os.environ.get("VPP_AMD_LIB", "libpolicygpu.so"))
     for i, combo in enumerate(combos):
         ms = float(np.median(times[i]))
-        print(json.dumps({"lib": name, "config": a.config, "counters": a.counters, "pre": a.pre, **dict(zip(keys, combo)), "ms": round(ms, 4),
+        print(json.dumps({"lib": name, "config": a.config, "counters": a.counters, "pre": a.pre, "ns": a.ns, **dict(zip(keys, combo)), "ms": round(ms, 4),
                           "gpps": round(n / ms / 1e6, 1), "GBps": round(n * bpt / ms / 1e6, 1),
                           "same_output": bool(torch.equal(outs[i], ref))}), flush=True)
 

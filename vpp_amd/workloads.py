@@ -333,8 +333,8 @@ def cluster_engine(device=0, n_ns=10, pods_per_ns=100, apps=5):
     return e, r, local, np.array(pool, np.uint32)
 
 
-def config3(device=0, n_tuples=125 << 20):
-    e, r, local, pool = cluster_engine(device)
+def config3(device=0, n_tuples=125 << 20, n_ns=10):
+    e, r, local, pool = cluster_engine(device, n_ns=n_ns)
     gen = dict(seed=SEEDS[3], ip_pool=pool, pool_pct=85, dst_pool_pct=88,
                port_pool=np.array(CLUSTER_PORTS, np.uint16), port_pool_pct=80, tcp_pct=60, udp_pct=30)
     return Workload(3, e, MODE_PERPOD, -1, gen, n_tuples,
@@ -342,8 +342,8 @@ def config3(device=0, n_tuples=125 << 20):
                     local_ifs=local)
 
 
-def config5(device=0, n_tuples=125 << 20):
-    e, r, local, pool = cluster_engine(device)
+def config5(device=0, n_tuples=125 << 20, n_ns=10):
+    e, r, local, pool = cluster_engine(device, n_ns=n_ns)
     gen = dict(seed=SEEDS[5], ip_pool=pool, pool_pct=85, dst_pool_pct=88,
                port_pool=np.array(CLUSTER_PORTS, np.uint16), port_pool_pct=80, tcp_pct=60, udp_pct=30)
     return Workload(5, e, MODE_CONN, -1, gen, n_tuples,
