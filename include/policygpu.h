@@ -145,7 +145,12 @@ pg_ctx* pg_create(int hip_device);
  * "node_path" (1/0: classify PERPOD / CONN through the node classifier when it exists,
  * default 1; 0 = per-table blobs and the IP hash), "node_stage_max_words" (largest node
  * image staged in LDS, default 16384), "block_stage" (workgroup size of LDS-staged
- * classify launches: 256, 512 or 1024; default 0 = per mode) */
+ * classify launches: 256, 512 or 1024; default 0 = per mode),
+ * "lc_lds" (table blobs of at least this many words are rebuilt with level-compressed
+ * 12/16/18-bit trie strides and keep them when the result still fits in LDS; default 4096,
+ * 0 = off; blobs too large for LDS are always level-compressed), "lc_dense12" (boundaries a
+ * subtree needs for a 12-bit stride, default 16), "lc_node" (1/0: level-compressed node
+ * tries, default 0) -- tables compiled afterwards */
 int pg_set_tuning(const char* key, int value);
 void pg_destroy(pg_ctx* ctx);
 const char* pg_last_error(const pg_ctx* ctx);

@@ -143,10 +143,19 @@ int pg_set_tuning(const char* key, int value) {
         set_root_bits_max((uint32_t)value);
         return PG_OK;
     }
-    if (std::string(key) == "lc_node" || std::string(key) == "lc_lds") {  // tables compiled afterwards
+    if (std::string(key) == "lc_dense12") {  // tables compiled afterwards
+        if (value < 1) return PG_EINVAL;
+        set_lc_dense12((uint32_t)value);
+        return PG_OK;
+    }
+    if (std::string(key) == "lc_node") {  // tables compiled afterwards
         if (value != 0 && value != 1) return PG_EINVAL;
-        if (std::string(key) == "lc_node") set_lc_node((uint32_t)value);
-        else set_lc_lds((uint32_t)value);
+        set_lc_node((uint32_t)value);
+        return PG_OK;
+    }
+    if (std::string(key) == "lc_lds") {  // min blob words for the LC rebuild, 0 = off
+        if (value < 0) return PG_EINVAL;
+        set_lc_lds((uint32_t)value);
         return PG_OK;
     }
     if (std::string(key) == "node_build" || std::string(key) == "node_root_bits") {  // tables compiled afterwards

@@ -10,7 +10,7 @@
 
 namespace pg {
 
-uint32_t g_lc_lds = 0;
+uint32_t g_lc_lds = 4096;  // LC rebuild of LDS-sized blobs of at least this many words (0 = off)
 void set_lc_lds(uint32_t on) { g_lc_lds = on; }
 
 // ---- compile one vpp_acl rule (aclengine_mock.go:510-649) --------------------------------
@@ -213,7 +213,7 @@ void Engine::compile() {
         hdr.dflt = (kActDeny << 30) | (NR + (uint32_t)t);
         bool ok = build_fast_table(h.rules.data() + hdr.rule_base, hdr.n_rules, hdr.rule_base, NR + (uint32_t)t, blob,
                                    1ull << 22, &an[t]);
-        if (ok && (blob.size() > kStageBlobWords || g_lc_lds)) {  // fewer dependent loads in dense subtrees
+        if (ok && (blob.size() > kStageBlobWords || (g_lc_lds && blob.size() >= g_lc_lds))) {  // fewer dependent loads in dense subtrees
             std::vector<uint32_t> lc;
             if (build_fast_table(h.rules.data() + hdr.rule_base, hdr.n_rules, hdr.rule_base, NR + (uint32_t)t, lc,
                                  1ull << 22, nullptr, true) &&

@@ -64,6 +64,7 @@ struct VecHash {
 // at least 8192 / 2048 / 256 interval boundaries: about the memory of the 8-bit levels they
 // replace, one or two dependent loads fewer.
 constexpr uint32_t kTrieFail = 0xFFFFFFFFu;
+uint32_t g_lc_dense12 = 16;  // boundaries in a child's span that earn it a 12-bit stride
 constexpr uint32_t kLcRootBits = 14;  // HBM-resident blobs: the root alone is staged in LDS (64 KiB)
 uint32_t build_trie(std::vector<uint32_t>& blob, const std::vector<uint64_t>& bnd, const std::vector<uint32_t>& cls,
                     uint32_t W, uint32_t s1, bool lc = false) {
@@ -100,7 +101,7 @@ uint32_t build_trie(std::vector<uint32_t>& blob, const std::vector<uint64_t>& bn
                 const size_t inside = (size_t)(std::lower_bound(bnd.begin(), bnd.end(), a + span) - bnd.begin()) - k - 1;
                 if (j.shift >= 18 && inside >= 8192) st = 18;
                 else if (j.shift >= 16 && inside >= 2048) st = 16;
-                else if (inside >= 256) st = 12;
+                else if (inside >= g_lc_dense12) st = 12;
             }
             uint32_t child = (uint32_t)blob.size();
             if ((uint64_t)child + (1ull << st) > kTrieChildMask) return kTrieFail;
@@ -150,6 +151,7 @@ void free_analysis(TableAnalysis* an) { delete an; }
 
 void set_root_bits_max(uint32_t bits) { g_root_bits_max = std::max<uint32_t>(4, std::min<uint32_t>(16, bits)); }
 void set_lc_node(uint32_t on) { g_lc_node = on; }
+void set_lc_dense12(uint32_t n) { g_lc_dense12 = n; }
 void set_node_tuning(uint32_t enable, uint32_t root_bits) {
     g_node_enable = enable;
     g_node_root_bits = std::max<uint32_t>(4, std::min<uint32_t>(16, root_bits));
