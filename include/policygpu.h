@@ -350,6 +350,62 @@ int pg_mock_renderer_test_traffic(pg_mock_renderer* r, const char* ns, const cha
                                   const char* src_ip, const char* dst_ip, int protocol, uint16_t src_port,
                                   uint16_t dst_port);
 
+/* ---- K8s policy cache and processor ------------------------------
+ * The KSR objects cross the boundary in their protobuf wire form (proto.Marshal of
+ * plugins/ksr/model/{pod,namespace,policy}.Pod / Namespace / Policy), so the Go side
+ * passes what it holds. policy.Policy_LabelSelector travels the same way for queries.
+ * cache.PolicyCacheAPI (plugins/policy/cache/cache_api.go:30-116, cache_impl.go),
+ * processor.PolicyProcessor (plugins/policy/processor/processor.go:34-527). Name lists come
+ * back sorted and '\n'-joined (the reference returns them in Go map order). */
+typedef struct pg_policy_cache pg_policy_cache;
+typedef struct pg_policy_processor pg_policy_processor;
+enum { PG_K8S_POD = 0, PG_K8S_NAMESPACE = 1, PG_K8S_POLICY = 2 };
+enum {
+    PG_Q_PODS_BY_LABEL_SELECTOR_INSIDE_NS = 0, /* arg = namespace, selector        */
+    PG_Q_PODS_BY_NS_LABEL_SELECTOR = 1,        /* selector                         */
+    PG_Q_PODS_BY_NAMESPACE = 2,                /* arg = namespace                  */
+    PG_Q_ALL_PODS = 3,
+    PG_Q_POLICIES_BY_POD = 4,                  /* arg = "ns/name"                  */
+    PG_Q_ALL_POLICIES = 5,
+    PG_Q_ALL_NAMESPACES = 6,
+    PG_Q_MATCH_LABEL_PODS_INSIDE_NS = 7,       /* arg = namespace, selector labels (match_label.go) */
+    PG_Q_PODS_BY_NS_LABELS = 8,                /* selector labels                  */
+    PG_Q_MATCH_EXPRESSION_PODS_INSIDE_NS = 9,  /* arg = namespace, selector expressions (match_expression.go) */
+    PG_Q_PODS_BY_NS_EXPRESSIONS = 10,          /* selector expressions             */
+    /* secondary indexes (podmap.go / namespacemap.go / policymap.go), arg = index value */
+    PG_Q_IDX_POD_LABEL = 11, PG_Q_IDX_POD_KEY = 12, PG_Q_IDX_POD_NS_LABEL = 13, PG_Q_IDX_POD_NS_KEY = 14,
+    PG_Q_IDX_NS_LABEL = 15, PG_Q_IDX_NS_KEY = 16, PG_Q_IDX_POLICY_LABEL = 17, PG_Q_IDX_POLICY_NS_LABEL = 18
+};
+pg_policy_cache* pg_policy_cache_new(void);
+void pg_policy_cache_free(pg_policy_cache* c);
+const char* pg_policy_cache_last_error(const pg_policy_cache* c);
+/* ConfigIndex.Register* / Unregister* (index only, no events); pb NULL = a nil object.
+ * unregister -> 1 found, 0 not */
+int pg_policy_cache_register(pg_policy_cache* c, int kind, const char* id, const uint8_t* pb, size_t len);
+int pg_policy_cache_unregister(pg_policy_cache* c, int kind, const char* id);
+/* Update (data_change.go): prev NULL = add, next NULL = delete, both = update; the
+ * watchers (processor) run inside. PG_EFAULT + last_error when a watcher fails. */
+int pg_policy_cache_update(pg_policy_cache* c, int kind, const uint8_t* prev, size_t prev_len, const uint8_t* next,
+                           size_t next_len);
+/* Resync (data_resync.go): the whole K8s state, n objects of the given kinds */
+int pg_policy_cache_resync(pg_policy_cache* c, const int* kinds, const uint8_t* const* objs, const size_t* lens,
+                           size_t n);
+/* Lookup{Pod,Namespace,Policy}: 1 found (wire bytes as registered -> out, *out_len; a nil
+ * object has *out_len = (size_t)-1), 0 not found */
+int pg_policy_cache_lookup(const pg_policy_cache* c, int kind, const char* id, uint8_t* out, size_t cap,
+                           size_t* out_len);
+/* name-list queries -> number of names; '\n'-joined into out when *out_len (bytes, no NUL)
+ * fits cap */
+int pg_policy_cache_query(const pg_policy_cache* c, int query, const char* arg, const uint8_t* selector,
+                          size_t selector_len, char* out, size_t cap, size_t* out_len);
+/* PolicyProcessor watching the cache and configuring cfg (which then looks pods up in the
+ * cache); pod_subnet = IPAM.PodSubnetThisNode() */
+pg_policy_processor* pg_policy_processor_new(pg_policy_cache* c, pg_configurator* cfg, const pg_ipnet* pod_subnet);
+void pg_policy_processor_free(pg_policy_processor* p);
+/* Process(resync, pods) with pods as "ns/name" */
+int pg_policy_processor_process(pg_policy_processor* p, int resync, const char* const* pods, size_t n);
+const char* pg_policy_processor_last_error(const pg_policy_processor* p);
+
 #ifdef __cplusplus
 }
 #endif

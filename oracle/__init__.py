@@ -10,6 +10,9 @@ This package restates, on the CPU and independently of the product code in
 * ``aclengine``  -- the mock ACL engine: ApplyTxn/PutACL/DelACL, evalACL with the
                     matched rule index, testConnection and Connection* (rows a10-a12).
 * ``mockrenderer`` -- mock/renderer TestTraffic (row a13).
+* ``configurator`` -- the policy configurator + mock renderer (row f1).
+* ``k8s_policy`` -- the K8s policy cache (label / namespace selector expansion) and the
+                    policy processor (row f3).
 * ``fast``       -- ctypes binding of ``oracle/oracle.c``: the same evalACL /
                     testConnection restated in C for bulk parity checks and the CPU
                     baseline leg of bench.py.

@@ -155,3 +155,78 @@ def test_cluster_via_configurator_equals_oracle_chain():
     assert sorted(o) == sorted(p) and len(o) > 3
     for name in o:
         assert o[name] == p[name], name
+
+
+def test_k8s_object_cluster_equals_oracle_chain():
+    """The cluster given as K8s objects (workloads.cluster_k8s: label / namespace selectors,
+    named ports, IPBlocks) through policy cache -> processor -> configurator -> ACL renderer
+    (workloads.cluster_engine_k8s) installs the same ACLs as the oracle chain (oracle cache ->
+    oracle processor -> oracle configurator -> oracle ACL renderer). SURVEY.md §8 f3."""
+    from oracle import configurator as OC
+    from oracle import gonet
+    from oracle import k8s_policy as OK
+    n_ns, pods_per_ns, apps = 4, 20, 5
+    e = R.Engine(0)
+    e.SetMainInterfaceName("GbE")
+    e.SetVxlanBVIIfName("VXLAN-BVI")
+    e.SetHostInterconnectIfName("VPP-Host")
+    import vpp_amd.workloads as WW
+    orig = WW._new_engine
+    WW._new_engine = lambda device: e
+    try:
+        e2, _, local, _, keep = W.cluster_engine_k8s(0, n_ns, pods_per_ns, apps)
+    finally:
+        WW._new_engine = orig
+    assert e2 is e
+    pods, nss, pols = W.cluster_k8s(n_ns, pods_per_ns, apps)
+    ocache = OK.PolicyCache()
+    ocfg = OC.PolicyConfigurator({}, W.NAT_LOOPBACK_IP)
+    mock = OC.MockRenderer()
+    ocfg.renderers.append(mock)
+    OK.PolicyProcessor(ocache, ocfg, W.NODE_POD_SUBNET)
+    ocache.resync(pods, nss, pols)
+    ids = ["%s/%s" % (p["Namespace"], p["Name"]) for p in pods]
+    remote = {i: p["IpAddress"].startswith("10.2.") for i, p in zip(ids, pods)}
+    assert sorted(mock.config) == sorted(i for i in ids if not remote[i])
+    setup = {"pod_ifs": {i: "tap-%s" % i.replace("/", "-") for i in ids if not remote[i]},
+             "host_interconnect": "VPP-Host", "main_if": "GbE", "other_ifs": [], "vxlan_bvi": "VXLAN-BVI",
+             "pods": [(i, p["IpAddress"], remote[i]) for i, p in zip(ids, pods)]}
+    ora = kd.OracleBackend()
+    ora.setup(setup)
+
+    def d(r):
+        net = lambda n: "" if n.is_empty() else gonet.ipnet_string(n)  # noqa: E731
+        return {"action": "PERMIT" if r.action else "DENY", "src": net(r.src), "dst": net(r.dst),
+                "proto": {0: "TCP", 1: "UDP", 2: "OTHER", 3: "ANY"}[r.protocol], "sport": r.src_port,
+                "dport": r.dst_port}
+    renders = [{"pod": p, "ip": gonet.ip_string(c[0].ip), "ingress": [d(r) for r in c[1]],
+                "egress": [d(r) for r in c[2]], "removed": False} for p, c in sorted(mock.config.items())]
+    assert ora.txn(True, renders) is None
+    o, p = oracle_acls(ora.engine), product_acls(e)
+    assert sorted(o) == sorted(p) and len(o) > 3
+    for name in o:
+        assert o[name] == p[name], name
+    assert sum(len(a["rules"]) for a in p.values()) > 1000
+
+
+@pytest.mark.parametrize("node", [True, False])
+def test_k8s_object_cluster_host_classify_equals_world(node):
+    """pg_classify's per-tuple code run on the host (PERPOD and CONN, node classifier and
+    per-table path) over the K8s-object cluster equals the C oracle through oracle.world."""
+    from vpp_amd._capi import MODE_CONN, MODE_PERPOD
+    e, _, local, pool, keep = W.cluster_engine_k8s(0, 4, 30, 5)
+    rng = np.random.default_rng(7)
+    n = 60000
+    src = pool[rng.integers(0, len(pool), n)]
+    dst = pool[rng.integers(0, len(pool), n)]
+    sport = rng.integers(0, 65536, n).astype(np.uint16)
+    dport = np.array(W.CLUSTER_PORTS + [8000, 8001, 8002, 8003, 8004], np.uint16)[rng.integers(0, 12, n)]
+    proto = np.array([6, 17, 1, 6, 17], np.uint8)[rng.integers(0, 5, n)]
+    wd = World(e, local, "VXLAN-BVI")
+    got = e.debug_classify_host(MODE_PERPOD, -1, src, dst, sport, dport, proto, node=node)
+    act, slot = wd.perpod(src, dst, dport, proto, threads=4)
+    assert ((got >> 30) == act.astype(np.uint32)).all() and ((got & 0x3FFFFFFF) == slot).all()
+    got = e.debug_classify_host(MODE_CONN, -1, src, dst, sport, dport, proto, node=node)
+    act, slot = wd.conn(src, dst, sport, dport, proto, threads=4)
+    assert ((got >> 30) == act.astype(np.uint32)).all() and ((got & 0x3FFFFFFF) == slot).all()
+    assert len(np.unique(act)) >= 2

@@ -286,6 +286,36 @@ def test_cluster_configs_gpu_vs_oracle(config):
     assert len(np.unique(got >> 30)) >= 2
 
 
+@pytest.mark.parametrize("mode", [MODE_PERPOD, MODE_CONN])
+def test_k8s_object_cluster_gpu_vs_oracle(mode):
+    """The cluster given as K8s objects (policy cache -> processor -> configurator -> renderer,
+    SURVEY.md §8 f3; 4 namespaces x 30 pods, namespace-wide selectors): 1M device-generated
+    tuples classified on the GPU, bit-exact against the C oracle through oracle.world."""
+    from oracle.world import World
+    from vpp_amd import workloads as W
+    e, r, local, pool, keep = W.cluster_engine_k8s(0, 4, 30, 5)
+    gen = dict(seed=0xC0DE0006, ip_pool=pool, pool_pct=85, dst_pool_pct=88,
+               port_pool=np.array(W.CLUSTER_PORTS + [8000, 8001, 8002, 8003, 8004], np.uint16), port_pool_pct=80,
+               tcp_pct=60, udp_pct=30)
+    b = D.TupleBatch(1 << 20, with_sport=(mode == MODE_CONN))
+    D.gen_tuples(e, b, **gen)
+    out = torch.empty(b.n, dtype=torch.int32, device="cuda")
+    cnt = torch.zeros(e.num_counter_slots(), dtype=torch.int64, device="cuda")
+    D.classify(e, mode, -1, b, out, counters=cnt)
+    torch.cuda.synchronize()
+    got = out.cpu().numpy().view(np.uint32)
+    src, dst, sport, dport, proto = b.numpy(b.n)
+    wd = World(e, local, "VXLAN-BVI")
+    if mode == MODE_PERPOD:
+        act, slot = wd.perpod(src, dst, dport, proto, threads=16)
+        assert np.array_equal(cnt.cpu().numpy(), np.bincount(got & 0x3FFFFFFF, minlength=cnt.numel()))
+    else:
+        act, slot = wd.conn(src, dst, sport, dport, proto, threads=16)
+    assert ((got >> 30) == act.astype(np.uint32)).all()
+    assert ((got & 0x3FFFFFFF) == slot).all()
+    assert len(np.unique(got >> 30)) >= 2
+
+
 def _classify_with(e, mode, b, node_path, stage_words=16384, counters=False):
     lib = R.lib
     assert lib.pg_set_tuning(b"node_path", node_path) == 0

@@ -158,6 +158,21 @@ _SIGS = {
                                          C.c_size_t]),
     "pg_mock_renderer_test_traffic": (C.c_int, [_P, C.c_char_p, C.c_char_p, C.c_int, C.c_char_p, C.c_char_p, C.c_int,
                                                 C.c_uint16, C.c_uint16]),
+    "pg_policy_cache_new": (_P, []),
+    "pg_policy_cache_free": (None, [_P]),
+    "pg_policy_cache_last_error": (C.c_char_p, [_P]),
+    "pg_policy_cache_register": (C.c_int, [_P, C.c_int, C.c_char_p, C.c_char_p, C.c_size_t]),
+    "pg_policy_cache_unregister": (C.c_int, [_P, C.c_int, C.c_char_p]),
+    "pg_policy_cache_update": (C.c_int, [_P, C.c_int, C.c_char_p, C.c_size_t, C.c_char_p, C.c_size_t]),
+    "pg_policy_cache_resync": (C.c_int, [_P, C.POINTER(C.c_int), C.POINTER(C.c_char_p), C.POINTER(C.c_size_t),
+                                         C.c_size_t]),
+    "pg_policy_cache_lookup": (C.c_int, [_P, C.c_int, C.c_char_p, C.c_char_p, C.c_size_t, C.POINTER(C.c_size_t)]),
+    "pg_policy_cache_query": (C.c_int, [_P, C.c_int, C.c_char_p, C.c_char_p, C.c_size_t, C.c_char_p, C.c_size_t,
+                                        C.POINTER(C.c_size_t)]),
+    "pg_policy_processor_new": (_P, [_P, _P, C.POINTER(pg_ipnet)]),
+    "pg_policy_processor_free": (None, [_P]),
+    "pg_policy_processor_process": (C.c_int, [_P, C.c_int, C.POINTER(C.c_char_p), C.c_size_t]),
+    "pg_policy_processor_last_error": (C.c_char_p, [_P]),
     "pg_classify_linear": (C.c_int, [_P, C.c_int, C.POINTER(pg_tuple_soa), C.c_uint64, _P, _P]),
     "pg_counters_device": (_P, [_P]),
     "pg_reset_counters": (C.c_int, [_P, _P]),

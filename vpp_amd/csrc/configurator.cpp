@@ -125,10 +125,10 @@ ContivRules PolicyConfiguratorTxn::generate_rules(int direction, const CfgPolici
             // IPs of the pod peers known to the cache
             std::vector<IPNet> peers;
             for (const PodID& peer : match.pods) {
-                auto pd = cfg->pod_data.find(peer);
-                if (pd == cfg->pod_data.end() || pd->second.empty()) continue;
+                std::string pd;
+                if (!cfg->pod_ip(peer, &pd) || pd.empty()) continue;
                 Bytes ip;
-                if (!parse_ip(pd->second, &ip)) continue;
+                if (!parse_ip(pd, &ip)) continue;
                 peers.push_back(one_host_subnet(ip));
             }
             // IPBlocks minus their excepts
@@ -208,15 +208,15 @@ std::string PolicyConfiguratorTxn::commit() {
         auto had = pod_ip_addresses.find(pod);
         const bool had_ip = had != pod_ip_addresses.end();
         IPNet pod_ip = had_ip ? had->second : IPNet();
-        auto pd = cfg->pod_data.find(pod);
-        if (pd == cfg->pod_data.end() || pd->second.empty()) {  // removed pod
+        std::string pd;
+        if (!cfg->pod_ip(pod, &pd) || pd.empty()) {  // removed pod
             if (!had_ip) continue;                              // already un-configured
             del = true;
             pod_ip_addresses.erase(pod);
         }
         if (!del) {
             Bytes ip;
-            if (!parse_ip(pd->second, &ip)) continue;  // invalid IP address: skipped
+            if (!parse_ip(pd, &ip)) continue;  // invalid IP address: skipped
             pod_ip = one_host_subnet(ip);
             pod_ip_addresses[pod] = pod_ip;
             CfgPolicies policies = kv.second;  // sorted by ID: the same set gives the same outcome

@@ -11,6 +11,7 @@
 //   utils.GetOneHostSubnet(FromIP)                          plugins/policy/utils/utils.go:270-291
 //   MockRenderer (NewTxn / Render / Commit / TestTraffic)   mock/renderer/renderer_mock.go:39-185
 #pragma once
+#include <functional>
 #include <map>
 #include <memory>
 #include <string>
@@ -86,8 +87,18 @@ struct MockRenderer : CfgRenderer {
 };
 
 struct PolicyConfigurator {
-    // policy cache (LookupPod): pods known to the cache and their IP address ("" = none)
+    // policy cache (LookupPod): pods known to the cache and their IP address ("" = none) ...
     std::map<PodID, std::string> pod_data;
+    // ... or, when set, the K8s policy cache itself (k8s.hpp PolicyCache, wired by the processor)
+    std::function<bool(const PodID&, std::string*)> lookup_pod;
+    // IP address of a pod known to the cache; false = unknown pod
+    bool pod_ip(const PodID& pod, std::string* ip) const {
+        if (lookup_pod) return lookup_pod(pod, ip);
+        auto it = pod_data.find(pod);
+        if (it == pod_data.end()) return false;
+        *ip = it->second;
+        return true;
+    }
     // IPAM.NatLoopbackIP(); empty Bytes = nil
     Bytes nat_loopback;
     std::vector<CfgRenderer*> renderers;

@@ -333,6 +333,91 @@ def cluster_engine(device=0, n_ns=10, pods_per_ns=100, apps=5):
     return e, r, local, np.array(pool, np.uint32)
 
 
+NODE_POD_SUBNET = "10.1.0.0/16"  # IPAM.PodSubnetThisNode() of the K8s-object cluster
+
+
+def cluster_k8s(n_ns=10, pods_per_ns=100, apps=5, remote_pct=10):
+    """The cluster as K8s objects (KSR model dicts, see vpp_amd/k8s.py) for the policy cache
+    and processor: label / namespace selectors, IPBlocks with excepts,
+    numbered and named ports. Pods ns<k>/app<a>-<j> on this node get 10.1.k.(j+1), the last
+    remote_pct % of every namespace run elsewhere (10.2.k.(j+1)).
+
+    Per (namespace k, app a), policy "app<a>-ingress" (PolicyType INGRESS) for pods app=app<a>:
+      from pods app=app<a+1> (same namespace)          TCP 80 and the named port "http"
+      from namespaces name=ns<k+1>                     TCP 443
+      from namespaces group In [g<(k+1)%3>] + pods with app NotIn [app0]   UDP 53
+      from 192.168.0.0/16 except 192.168.10.0/24       TCP 22
+    and for app0 pods "app0-egress" (EGRESS): TCP 443 anywhere, UDP 53 to 10.96.0.10/32,
+    the named port "http" of namespace ns<k>'s pods."""
+    lbl = lambda k, v: {"Key": k, "Value": v}  # noqa: E731
+    namespaces = [{"Name": "ns%d" % k, "Label": [lbl("name", "ns%d" % k), lbl("group", "g%d" % (k % 3))]}
+                  for k in range(n_ns)]
+    pods = []
+    for k in range(n_ns):
+        for j in range(pods_per_ns):
+            remote = j >= pods_per_ns * (100 - remote_pct) // 100
+            pods.append({"Name": "app%d-%d" % (j % apps, j), "Namespace": "ns%d" % k,
+                         "Label": [lbl("app", "app%d" % (j % apps)), lbl("tier", "t%d" % (j % 2))],
+                         "IpAddress": "10.%d.%d.%d" % (2 if remote else 1, k, j + 1),
+                         "Container": [{"Name": "main", "Port": [{"Name": "http", "ContainerPort": 8000 + j % apps}]}]})
+    tcp = lambda n: {"Protocol": 0, "Port": {"Type": 0, "Number": n}}  # noqa: E731
+    udp = lambda n: {"Protocol": 1, "Port": {"Type": 0, "Number": n}}  # noqa: E731
+    named = {"Protocol": 0, "Port": {"Type": 1, "Name": "http"}}
+    policies = []
+    for k in range(n_ns):
+        for a in range(apps):
+            policies.append({
+                "Name": "app%d-ingress" % a, "Namespace": "ns%d" % k, "PolicyType": 1,
+                "Pods": {"MatchLabel": [lbl("app", "app%d" % a)]},
+                "IngressRule": [
+                    {"Port": [tcp(80), named], "From": [{"Pods": {"MatchLabel": [lbl("app", "app%d" % ((a + 1) % apps))]}}]},
+                    {"Port": [tcp(443)], "From": [{"Namespaces": {"MatchLabel": [lbl("name", "ns%d" % ((k + 1) % n_ns))]}}]},
+                    {"Port": [udp(53)], "From": [{
+                        "Namespaces": {"MatchExpression": [{"Key": "group", "Operator": 0, "Value": ["g%d" % ((k + 1) % 3)]}]},
+                        "Pods": {"MatchExpression": [{"Key": "app", "Operator": 1, "Value": ["app0"]}]}}]},
+                    {"Port": [tcp(22)], "From": [{"IpBlock": {"Cidr": "192.168.0.0/16", "Except": ["192.168.10.0/24"]}}]},
+                ]})
+        policies.append({
+            "Name": "app0-egress", "Namespace": "ns%d" % k, "PolicyType": 2,
+            "Pods": {"MatchLabel": [lbl("app", "app0")]},
+            "EgressRule": [
+                {"Port": [tcp(443)], "To": []},
+                {"Port": [udp(53)], "To": [{"IpBlock": {"Cidr": "10.96.0.10/32"}}]},
+                {"Port": [named], "To": [{"Namespaces": {"MatchLabel": [lbl("name", "ns%d" % k)]}}]},
+            ]})
+    return pods, namespaces, policies
+
+
+def cluster_engine_k8s(device=0, n_ns=10, pods_per_ns=100, apps=5):
+    """The K8s-object cluster through the whole control path of the reference: policy cache
+    (Resync) -> policy processor (selector expansion, named ports, this node's pods) ->
+    policy configurator -> GPU ACL renderer -> engine. Returns (engine, renderer, local
+    interfaces {IPv4: TAP}, tuple IP pool, (cache, processor, configurator))."""
+    from . import configurator as CF
+    from . import k8s as K
+    e = _new_engine(device)
+    pods, namespaces, policies = cluster_k8s(n_ns, pods_per_ns, apps)
+    local = {}
+    for p in pods:
+        pid = "%s/%s" % (p["Namespace"], p["Name"])
+        remote = p["IpAddress"].startswith("10.2.")
+        if not remote:
+            ifn = "tap-%s" % pid.replace("/", "-")
+            e.SetPodIfName(pid, ifn)
+            local[ip_u32(p["IpAddress"])] = ifn
+        e.RegisterPod(pid, p["IpAddress"], remote)
+    r = R.Renderer(e)
+    cfg = CF.PolicyConfigurator()
+    cfg.SetNatLoopbackIP(NAT_LOOPBACK_IP)
+    assert cfg.RegisterRenderer(r) is None
+    cache = K.PolicyCache()
+    proc = K.PolicyProcessor(cache, cfg, NODE_POD_SUBNET)
+    err = cache.Resync(pods, namespaces, policies)
+    assert err is None, err
+    pool = [ip_u32(p["IpAddress"]) for p in pods] + [ip_u32(x) for x in INTERNET_HOSTS] * 10
+    return e, r, local, np.array(pool, np.uint32), (cache, proc, cfg)
+
+
 def config3(device=0, n_tuples=125 << 20, n_ns=10):
     e, r, local, pool = cluster_engine(device, n_ns=n_ns)
     gen = dict(seed=SEEDS[3], ip_pool=pool, pool_pct=85, dst_pool_pct=88,
