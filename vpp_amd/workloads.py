@@ -20,7 +20,7 @@ import numpy as np
 from . import renderer as R
 from ._capi import MODE_CONN, MODE_PERPOD, MODE_SINGLE
 
-SEEDS = {1: 0xC0DE0001, 2: 0xC0DE0002, 3: 0xC0DE0003, 4: 0xC0DE0004, 5: 0xC0DE0005}
+SEEDS = {1: 0xC0DE0001, 2: 0xC0DE0002, 3: 0xC0DE0003, 4: 0xC0DE0004, 5: 0xC0DE0005, 6: 0xC0DE0006}
 POPULAR_PORTS = [22, 53, 67, 80, 81, 161, 162, 443, 514, 8080]
 
 
@@ -436,6 +436,20 @@ def config5(device=0, n_tuples=125 << 20, n_ns=10):
                     local_ifs=local, counters=True)
 
 
+def config6(device=0, n_tuples=125 << 20, n_ns=10):
+    """Config 3's shape given as K8s objects: namespace-wide selectors make
+    the rule lists ~6.7x longer (64.6k rules in 52 tables)."""
+    e, r, local, pool, keep = cluster_engine_k8s(device, n_ns=n_ns)
+    gen = dict(seed=SEEDS[6], ip_pool=pool, pool_pct=85, dst_pool_pct=88,
+               port_pool=np.array(CLUSTER_PORTS + [8000, 8001, 8002, 8003, 8004], np.uint16), port_pool_pct=80,
+               tcp_pct=60, udp_pct=30)
+    w = Workload(6, e, MODE_PERPOD, -1, gen, n_tuples,
+                 "K8s objects (10 ns x 100 pods, label/namespace selectors) -> policy cache / processor / "
+                 "configurator -> per-pod tables, evalACL on the dst interface", r, local_ifs=local)
+    w.control = keep  # the cache / processor / configurator stay alive with the engine
+    return w
+
+
 def table_histogram(e):
     """rules per table -> number of tables (config 3's table-size histogram)."""
     h = {}
@@ -445,4 +459,4 @@ def table_histogram(e):
     return dict(sorted(h.items()))
 
 
-CONFIGS = {1: config1, 2: config2, 3: config3, 4: config4, 5: config5}
+CONFIGS = {1: config1, 2: config2, 3: config3, 4: config4, 5: config5, 6: config6}
