@@ -150,7 +150,10 @@ pg_ctx* pg_create(int hip_device);
  * 12/16/18-bit trie strides and keep them when the result still fits in LDS; default 4096,
  * 0 = off; blobs too large for LDS are always level-compressed), "lc_dense12" (boundaries a
  * subtree needs for a 12-bit stride, default 16), "lc_node" (1/0: level-compressed node
- * tries, default 0) -- tables compiled afterwards */
+ * tries, default 0), "pair" (1/0: the PAIR structure -- src x dst classes, then x key
+ * classes -- for tables the cross product cannot take, default 1; 0 = candidate lists;
+ * 2 = wherever it fits, for tests)
+ * -- tables compiled afterwards */
 int pg_set_tuning(const char* key, int value);
 void pg_destroy(pg_ctx* ctx);
 const char* pg_last_error(const pg_ctx* ctx);

@@ -65,9 +65,22 @@ def test_dst_specific_rules_use_lists():
     check(e, "g", rules, tup)
 
 
+class tuning:
+    """pg_set_tuning for the tables compiled inside the block"""
+
+    def __init__(self, key, value, default):
+        self.k, self.v, self.d = key.encode(), value, default
+
+    def __enter__(self):
+        assert R.lib.pg_set_tuning(self.k, self.v) == 0
+
+    def __exit__(self, *a):
+        R.lib.pg_set_tuning(self.k, self.d)
+
+
 def test_large_table_uses_candidate_mode():
     rules = []
-    for k in range(20000):       # > 16384 rules: no cross product
+    for k in range(20000):       # > 16384 rules, 20k src x 1k key classes: no product fits
         rules.append({"action": k % 2, "src": "10.%d.%d.0/24" % (k // 256, k % 256), "dst": "",
                       "udp": {"src": [0, 65535], "dst": [k % 1000, k % 1000 + 5]}})
     e = engine_with({"big": rules})
@@ -75,6 +88,47 @@ def test_large_table_uses_candidate_mode():
     anchors = [(10 << 24) | (k << 8) for k in range(0, 20000, 37)]
     tup = fz.rand_tuples(np.random.default_rng(9), 30000, anchors)
     check(e, "big", rules, tup)
+
+
+def test_long_dst_lists_use_pair_mode():
+    """global-table shape with long dst lists (egress to many pod /32s per port): PAIR mode,
+    and the same verdicts with it disabled (cross product + dst lists)"""
+    rnd = random.Random(11)
+    pods = [0x0A010000 | k for k in range(1, 400)]
+    rules = []
+    for s in range(12):
+        src = "10.1.0.%d/32" % (s + 1)
+        rules.append({"action": 1, "src": src, "dst": "", "tcp": {"src": [0, 65535], "dst": [443, 443]}})
+        for p in rnd.sample(pods, 300):
+            port = rnd.choice([8000, 8001, 8002])
+            rules.append({"action": 1, "src": src, "dst": "%d.%d.%d.%d/32" % (p >> 24, p >> 16 & 255, p >> 8 & 255,
+                                                                            p & 255),
+                          "tcp": {"src": [0, 65535], "dst": [port, port]}})
+        rules.append({"action": 1, "src": src, "dst": "10.96.0.10/32", "udp": {"src": [0, 65535], "dst": [53, 53]}})
+        rules.append({"action": 0, "src": src, "dst": ""})
+    rules.append({"action": 1, "src": "", "dst": ""})
+    anchors = pods[:40] + [0x0A010001 + k for k in range(12)] + [0x0A60000A]
+    tup = fz.rand_tuples(np.random.default_rng(11), 40000, anchors)
+    for pair, want in ((1, "pair"), (0, "cross+lists")):
+        with tuning("pair", pair, 1):
+            e = engine_with({"g": rules})
+            assert e.table_stats(0)["structure"] == want
+        check(e, "g", rules, tup)
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_random_weird_acls_pair_mode(seed):
+    """every random weird ACL compiled into PAIR mode (pair = 2) walks to evalACL's verdicts"""
+    rnd = random.Random(100 + seed)
+    acls = {"t%d" % k: fz.rand_acl(rnd, rnd.choice([1, 3, 12, 60, 250]), fz.ANCHORS, weird=True,
+                                   tail=rnd.choice([None, "deny", "permit"])) for k in range(3)}
+    with tuning("pair", 2, 1):
+        e = engine_with(acls)
+        e.table_stats(0)  # compiles the tables under the tuning
+    tup = fz.rand_tuples(np.random.default_rng(100 + seed), 20000, fz.ANCHORS, any_pct=0.03)
+    for n, r in acls.items():
+        assert e.table_stats(e.table_id(n))["structure"] in ("pair", "linear")
+        check(e, n, r, tup)
 
 
 def test_empty_and_catch_all_tables():

@@ -19,7 +19,8 @@
 
 namespace pg {
 
-constexpr uint32_t kFlagCross = 1u, kFlagLists = 2u, kFlagCand = 4u, kFlagLinear = 8u;
+constexpr uint32_t kFlagCross = 1u, kFlagLists = 2u, kFlagCand = 4u, kFlagLinear = 8u, kFlagPair = 16u;
+constexpr uint32_t kPairHdr = 12u;  // PAIR blob header words: dst root, d1, pair table, n_dst_classes
 constexpr uint32_t kLeaf = 0x80000000u;
 // non-leaf trie entry: child block offset (words) | child stride << kTrieStrideShift
 constexpr uint32_t kTrieStrideShift = 26u, kTrieChildMask = (1u << kTrieStrideShift) - 1u;
@@ -66,28 +67,42 @@ PG_HD bool rec_match(const W4& r, uint32_t dst, uint32_t key) {
 template <bool PRED = false, class L, class L0, int Q>
 PG_HD void blob_walk(const L (&ld)[Q], const L0 (&ld0)[Q], const BlobTab (&tb)[Q], const bool (&on)[Q],
                      const uint32_t (&src)[Q], const uint32_t (&dst)[Q], const uint32_t (&key)[Q], uint32_t (&w)[Q]) {
-    uint32_t es[Q], ek[Q], ss[Q], sk[Q];
+    uint32_t es[Q], ek[Q], ss[Q], sk[Q], ed[Q], sd[Q];
     PG_UNROLL
     for (int j = 0; j < Q; j++) {
-        es[j] = ek[j] = kLeaf;
-        ss[j] = sk[j] = 0;
+        es[j] = ek[j] = ed[j] = kLeaf;
+        ss[j] = sk[j] = sd[j] = 0;
         if (on[j]) {
             ss[j] = 32u - ((tb[j].fsk >> 8) & 0xFFu);
             es[j] = ld0[j].u32(kSrcRoot + (src[j] >> ss[j]));
-            if (tb[j].fsk & kFlagCross) {
-                sk[j] = 18u - (tb[j].fsk >> 16);
+            if (tb[j].fsk & (kFlagCross | kFlagPair)) {
+                sk[j] = 18u - ((tb[j].fsk >> 16) & 0xFFu);
                 ek[j] = ld[j].u32(tb[j].kroot + (key[j] >> sk[j]));
             }
         }
     }
-    // descend both multibit tries (root stride, then 8-bit strides) of all Q tuples together
+    // PAIR tables: the dst trie too (its root and stride are in the blob header)
+    PG_UNROLL
+    for (int j = 0; j < Q; j++) {
+        if (on[j] && (tb[j].fsk & kFlagPair)) {
+            const W2 h = ld[j].u2(kPairHdr);
+            sd[j] = 32u - h.y;
+            ed[j] = ld[j].u32(h.x + (dst[j] >> sd[j]));
+        }
+    }
+    // descend the multibit tries (root stride, then each node's stride) of all Q tuples together
     for (;;) {
         bool more = false;
         PG_UNROLL
-        for (int j = 0; j < Q; j++) more |= !(es[j] & ek[j] & kLeaf);
+        for (int j = 0; j < Q; j++) more |= !(es[j] & ek[j] & ed[j] & kLeaf);
         if (!more) break;
         PG_UNROLL
         for (int j = 0; j < Q; j++) {
+            if (!(ed[j] & kLeaf)) {
+                const uint32_t st = trie_stride(ed[j]);
+                sd[j] -= st;
+                ed[j] = ld[j].u32(trie_child(ed[j]) + ((dst[j] >> sd[j]) & ((1u << st) - 1u)));
+            }
             if (PRED) {
                 const bool ds = !(es[j] & kLeaf), dk = !(ek[j] & kLeaf);
                 const uint32_t ts = ds ? trie_stride(es[j]) : 0u, tk = dk ? trie_stride(ek[j]) : 0u;
@@ -122,7 +137,11 @@ PG_HD void blob_walk(const L (&ld)[Q], const L0 (&ld0)[Q], const BlobTab (&tb)[Q
         pos[j] = 0;
         if (!on[j]) continue;
         const uint32_t sc = es[j] & ~kLeaf;
-        if (tb[j].fsk & kFlagCross) {
+        if (tb[j].fsk & kFlagPair) {  // (src, dst) -> pair class -> x key class -> verdict
+            const W2 h = ld[j].u2(kPairHdr + 2u);
+            const uint32_t pc = ld[j].u32(h.x + sc * h.y + (ed[j] & ~kLeaf));
+            w[j] = ld[j].u32(tb[j].xoff + pc * tb[j].nkc + (ek[j] & ~kLeaf));
+        } else if (tb[j].fsk & kFlagCross) {
             const uint32_t idx = sc * tb[j].nkc + (ek[j] & ~kLeaf);
             if (!(tb[j].fsk & kFlagLists)) {
                 w[j] = ld[j].u32(tb[j].xoff + idx);

@@ -148,6 +148,11 @@ int pg_set_tuning(const char* key, int value) {
         set_lc_dense12((uint32_t)value);
         return PG_OK;
     }
+    if (std::string(key) == "pair") {  // tables compiled afterwards
+        if (value < 0 || value > 2) return PG_EINVAL;
+        set_pair_enable((uint32_t)value);
+        return PG_OK;
+    }
     if (std::string(key) == "lc_node") {  // tables compiled afterwards
         if (value != 0 && value != 1) return PG_EINVAL;
         set_lc_node((uint32_t)value);
@@ -438,7 +443,7 @@ int pg_table_stats(pg_ctx* ctx, int table_id, uint32_t* flags, uint32_t* blob_by
     if (flags) *flags = hd.fsk & 0xFFu;
     if (blob_bytes) *blob_bytes = words * 4;
     if (n_src_classes) *n_src_classes = words ? b[10] : 0;
-    if (n_key_classes) *n_key_classes = (words && (hd.fsk & kFlagCross)) ? b[7] : 0;
+    if (n_key_classes) *n_key_classes = (words && (hd.fsk & (kFlagCross | kFlagPair))) ? b[7] : 0;
     return PG_OK;
     GUARD_END(ctx)
 }

@@ -115,6 +115,7 @@ bool build_node(HostTableSet& h, const std::vector<TableAnalysis*>& an, const st
                 const NodePod& node_end);
 void set_root_bits_max(uint32_t bits);  // cap of the tries' root stride (4..16)
 void set_node_tuning(uint32_t enable, uint32_t root_bits);
+void set_pair_enable(uint32_t on);  // PAIR mode for tables CROSS cannot take (tables compiled afterwards)
 void set_lc_node(uint32_t on);  // level-compressed node IPv4 trie (tables compiled afterwards)
 void set_lc_lds(uint32_t on);
 void set_lc_dense12(uint32_t n);  // level-compression threshold for 12-bit strides (default 256)   // level-compressed tries also for LDS-staged blobs that stay <= 64 KiB

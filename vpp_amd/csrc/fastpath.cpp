@@ -23,12 +23,14 @@
 //
 // Blob words (u32), all offsets relative to the blob start so it can be read from HBM or
 // copied verbatim into LDS:
-//   [0]  flags: 1 = CROSS, 2 = LISTS, 4 = CAND
+//   [0]  flags: 1 = CROSS, 2 = LISTS, 4 = CAND, 16 = PAIR
 //   [1]  default verdict (DENY << 30 | table's default slot)
 //   [2]  src trie root (always 16)   [3] s1     [4] key trie root   [5] k1
 //   [6]  CROSS: cross table (u32 verdicts, or LISTS: u2 {verdict, first record | 0});
 //        CAND: first record
-//   [7]  n_key_classes   [10] n_src_classes   [8, 9, 11..15] reserved
+//   [7]  n_key_classes   [10] n_src_classes   [8, 9, 11] reserved
+//   PAIR (flag 16): [6] pair x key verdicts, [12] dst trie root, [13] d1, [14] (src class x
+//        dst class) -> pair class table, [15] n_dst_classes
 //   records (16 B, blobwalk.hpp): {dnet, klo | dst prefix length << 18, khi, verdict}; every
 //   list ends with a match-all record carrying the fall-through verdict.
 #include <algorithm>
@@ -128,6 +130,10 @@ bool live(const DevRule& r) { return r.klo <= r.khi; }  // can match a TCP/UDP/O
 
 uint32_t g_node_enable = 1;
 uint32_t g_lc_node = 0;  // level-compressed node tries (LDS image)
+uint32_t g_pair_enable = 1;  // PAIR mode for tables CROSS cannot take (else CAND); 2 = always
+constexpr uint32_t kPairMaxRules = 1u << 16;
+constexpr uint64_t kPairBudget = 1ull << 22;  // entries of each PAIR phase table (16 MiB)
+constexpr size_t kPairListMin = 16;  // CROSS dst lists longer than this: PAIR instead
 uint32_t g_node_root_bits = 12;           // node IPv4 trie root: 2^12 words = 16 KiB
 constexpr uint64_t kNodeCrossBudget = 1ull << 25;  // node cross entries (128 MiB)
 
@@ -151,6 +157,7 @@ void free_analysis(TableAnalysis* an) { delete an; }
 
 void set_root_bits_max(uint32_t bits) { g_root_bits_max = std::max<uint32_t>(4, std::min<uint32_t>(16, bits)); }
 void set_lc_node(uint32_t on) { g_lc_node = on; }
+void set_pair_enable(uint32_t on) { g_pair_enable = on; }
 void set_lc_dense12(uint32_t n) { g_lc_dense12 = n; }
 void set_node_tuning(uint32_t enable, uint32_t root_bits) {
     g_node_enable = enable;
@@ -234,14 +241,15 @@ bool build_fast_table(const DevRule* rules, uint32_t n, uint32_t rule_base, uint
     blob[10] = nsc;
 
     // ---- key classes and the cross product, if it fits ---------------------------------------
-    bool cross = n <= 16384;
+    bool cross = n <= 16384 && g_pair_enable != 2;  // pair = 2: PAIR wherever it fits (tests)
     std::vector<uint64_t> kb{0};
     std::vector<uint32_t> kseg_cls;
     std::vector<std::vector<uint32_t>> key_sets;  // sorted rule indices covering the segment
     std::vector<uint32_t> cverd;
     std::vector<std::vector<uint32_t>> clist;
     bool lists = false;
-    if (cross) {
+    size_t max_list = 0;
+    auto compute_keys = [&]() {
         for (uint32_t i = 0; i < n; i++) {
             if (!live(rules[i])) continue;
             kb.push_back(rules[i].klo);
@@ -272,6 +280,9 @@ bool build_fast_table(const DevRule* rules, uint32_t n, uint32_t rule_base, uint
             }
             kseg_cls[k] = it->second;
         }
+    };
+    if (cross) {
+        compute_keys();
         if ((uint64_t)nsc * key_sets.size() > cross_budget) cross = false;
     }
     if (cross) {
@@ -301,10 +312,139 @@ bool build_fast_table(const DevRule* rules, uint32_t n, uint32_t rule_base, uint
                     break;
                 }
                 if (!L.empty()) lists = true;
+                max_list = std::max<size_t>(max_list, L.size());
             }
         }
     }
 
+    // a failed PAIR attempt may have appended to the blob: back to the bare header
+    auto blob_header_only = [&]() {
+        blob.resize(16);
+        blob[0] = 0;
+    };
+    // ---- PAIR mode: src class x dst class -> pair class, pair class x key class -> verdict ----
+    // For tables whose dst-specific rules are too many for CROSS dst lists (or that exceed
+    // its rule bound): the third field gets its own trie and the cross product is taken in
+    // two phases (RFC's phase-2 combination): each (src class, dst class) maps to the class
+    // of its ordered rule list (the src list filtered by dst, truncated at the first rule
+    // matching every key), and that class times the key class to the first rule covering it.
+    auto try_pair = [&]() -> bool {
+        if (key_sets.empty()) compute_keys();
+        const uint32_t nkc = (uint32_t)key_sets.size();
+        // dst elementary intervals, classed by the set of dst-specific rules covering them
+        std::vector<uint64_t> db{0};
+        std::vector<std::pair<uint64_t, uint32_t>> dst_s, dst_e;
+        for (uint32_t i = 0; i < n; i++) {
+            const DevRule& r = rules[i];
+            if (r.dmask == 0 || !live(r)) continue;
+            db.push_back(r.dnet);
+            dst_s.push_back({r.dnet, i});
+            const uint64_t end = (uint64_t)r.dnet + (uint64_t)(~r.dmask) + 1ull;
+            if (end < (1ull << 32)) {
+                db.push_back(end);
+                dst_e.push_back({end, i});
+            }
+        }
+        std::sort(db.begin(), db.end());
+        db.erase(std::unique(db.begin(), db.end()), db.end());
+        std::sort(dst_s.begin(), dst_s.end());
+        std::sort(dst_e.begin(), dst_e.end());
+        std::set<uint32_t> dact;
+        std::unordered_map<std::vector<uint32_t>, uint32_t, VecHash> dst_cls_of;
+        std::vector<std::vector<uint32_t>> dst_sets;
+        std::vector<uint32_t> dint_cls(db.size());
+        size_t a = 0, b = 0;
+        for (size_t k = 0; k < db.size(); k++) {
+            while (b < dst_e.size() && dst_e[b].first <= db[k]) dact.erase(dst_e[b++].second);
+            while (a < dst_s.size() && dst_s[a].first <= db[k]) dact.insert(dst_s[a++].second);
+            std::vector<uint32_t> v(dact.begin(), dact.end());
+            auto it = dst_cls_of.find(v);
+            if (it == dst_cls_of.end()) {
+                it = dst_cls_of.emplace(v, (uint32_t)dst_sets.size()).first;
+                dst_sets.push_back(std::move(v));
+            }
+            dint_cls[k] = it->second;
+        }
+        const uint32_t ndc = (uint32_t)dst_sets.size();
+        const size_t words = (n + 63) / 64;
+        uint64_t work = 0;
+        for (uint32_t sc = 0; sc < nsc; sc++) work += (uint64_t)src_lists[sc].size() * ndc;
+        if ((uint64_t)nsc * ndc <= kPairBudget && (uint64_t)ndc * words <= (1ull << 26) && work <= (1ull << 30)) {
+            std::vector<uint64_t> dbits((size_t)ndc * words, 0);
+            for (uint32_t d = 0; d < ndc; d++)
+                for (uint32_t r : dst_sets[d]) dbits[(size_t)d * words + r / 64] |= 1ull << (r % 64);
+            std::vector<uint32_t> pmap((size_t)nsc * ndc);
+            std::unordered_map<std::vector<uint32_t>, uint32_t, VecHash> pc_of;
+            std::vector<std::vector<uint32_t>> pc_lists;
+            std::vector<uint32_t> L;
+            for (uint32_t sc = 0; sc < nsc; sc++)
+                for (uint32_t d = 0; d < ndc; d++) {
+                    const uint64_t* bits = &dbits[(size_t)d * words];
+                    L.clear();
+                    for (uint32_t r : src_lists[sc]) {
+                        if (rules[r].dmask != 0 && !((bits[r / 64] >> (r % 64)) & 1)) continue;
+                        L.push_back(r);
+                        if (rules[r].klo == 0 && rules[r].khi == kKeyMax) break;  // every key matches
+                    }
+                    auto it = pc_of.find(L);
+                    if (it == pc_of.end()) {
+                        it = pc_of.emplace(L, (uint32_t)pc_lists.size()).first;
+                        pc_lists.push_back(L);
+                    }
+                    pmap[(size_t)sc * ndc + d] = it->second;
+                }
+            const uint32_t npc = (uint32_t)pc_lists.size();
+            if ((uint64_t)npc * nkc <= kPairBudget) {
+                std::vector<uint64_t> kbits((size_t)nkc * words, 0);
+                for (uint32_t c = 0; c < nkc; c++)
+                    for (uint32_t r : key_sets[c]) kbits[(size_t)c * words + r / 64] |= 1ull << (r % 64);
+                std::vector<uint32_t> xv((size_t)npc * nkc, dflt);
+                for (uint32_t p = 0; p < npc; p++)
+                    for (uint32_t c = 0; c < nkc; c++) {
+                        const uint64_t* bits = &kbits[(size_t)c * words];
+                        for (uint32_t r : pc_lists[p])
+                            if ((bits[r / 64] >> (r % 64)) & 1) {
+                                xv[(size_t)p * nkc + c] = verdict(r);
+                                break;
+                            }
+                    }
+                const uint32_t s1 = std::min<uint32_t>(pick_stride(sb.size(), 32), lc ? kLcRootBits : 32u);
+                if (build_trie(blob, sb, sint_cls, 32, s1, lc) != kSrcRoot) return false;
+                const uint32_t k1 = pick_stride(kb.size(), 18);
+                const uint32_t kroot = build_trie(blob, kb, kseg_cls, 18, k1, lc);
+                const uint32_t d1 = pick_stride(db.size(), 32);
+                const uint32_t droot = kroot == kTrieFail ? kTrieFail : build_trie(blob, db, dint_cls, 32, d1, lc);
+                if (droot == kTrieFail) return false;
+                while (blob.size() % 4) blob.push_back(0);
+                const size_t poff = blob.size();
+                blob.insert(blob.end(), pmap.begin(), pmap.end());
+                while (blob.size() % 4) blob.push_back(0);
+                const size_t xoff = blob.size();
+                blob.insert(blob.end(), xv.begin(), xv.end());
+                if (blob.size() >= 0x7FFFFFF0u) return false;
+                blob[0] = kFlagPair;
+                blob[2] = kSrcRoot;
+                blob[3] = s1;
+                blob[4] = kroot;
+                blob[5] = k1;
+                blob[6] = (uint32_t)xoff;
+                blob[7] = nkc;
+                blob[10] = nsc;
+                blob[12] = droot;
+                blob[13] = d1;
+                blob[14] = (uint32_t)poff;
+                blob[15] = ndc;
+                return true;
+            }
+        }
+        return false;
+    };
+
+    // long dst lists: PAIR's two lookups beat a record scan (unless it does not fit)
+    if (cross && lists && max_list > kPairListMin && g_pair_enable && n <= kPairMaxRules) {
+        if (try_pair()) return true;
+        blob_header_only();
+    }
     if (cross) {
         const uint32_t nkc = (uint32_t)key_sets.size();
         const uint32_t s1 = std::min<uint32_t>(pick_stride(sb.size(), 32), lc ? kLcRootBits : 32u);
@@ -356,6 +496,9 @@ bool build_fast_table(const DevRule* rules, uint32_t n, uint32_t rule_base, uint
         }
         return true;
     }
+
+    if (!cross && g_pair_enable && n <= kPairMaxRules && try_pair()) return true;
+    blob_header_only();
 
     // ---- candidate mode: src trie leaves point at the class's record list -------------------
     std::vector<uint32_t> first_rec(nsc);
