@@ -24,6 +24,9 @@ namespace pg {
 #else
 #define PG_NOINLINE inline
 #endif
+#ifndef PG_NODE_FB_Q1  // node kernels: per-table fallback one tuple at a time
+#define PG_NODE_FB_Q1 1
+#endif
 
 // TCP -> port, UDP -> 0x10000 | port, OTHER -> 0x20000, anything else -> 0x30000 (branch-free)
 PG_HD uint32_t pkt_key(uint32_t proto, uint32_t port) {
@@ -350,6 +353,20 @@ struct NodeEval {
         PG_UNROLL
         for (int j = 0; j < Q; j++) anyfb |= fb[j];
         if (anyfb) {
+#if PG_NODE_FB_Q1
+            // the per-table path one tuple at a time: it is rare here (tables the node does
+            // not cover, ANY-protocol packets), and a lockstep walk of Q tuples would size the
+            // whole kernel's register allocation
+            for (int j = 0; j < Q; j++) {
+                if (!fb[j]) continue;
+                const DevTable tab1[1] = {load_tab(T.tabs, t[j])};
+                const bool on1[1] = {true};
+                const uint32_t a1[1] = {a[j]}, b1[1] = {b[j]}, k1[1] = {k[j]};
+                uint32_t w1[1];
+                eval_q(T, T.blobs, tab1, on1, a1, b1, k1, w1);
+                w[j] = w1[0];
+            }
+#else
             DevTable tab[Q];
             PG_UNROLL
             for (int j = 0; j < Q; j++) tab[j] = fb[j] ? load_tab(T.tabs, t[j]) : DevTable{};
@@ -358,6 +375,7 @@ struct NodeEval {
             PG_UNROLL
             for (int j = 0; j < Q; j++)
                 if (fb[j]) w[j] = wf[j];
+#endif
         }
     }
 };
