@@ -409,6 +409,79 @@ void pg_policy_processor_free(pg_policy_processor* p);
 int pg_policy_processor_process(pg_policy_processor* p, int resync, const char* const* pods, size_t n);
 const char* pg_policy_processor_last_error(const pg_policy_processor* p);
 
+/* ---- VPPTCP renderer and VPP session-rule tables -------------------
+ * The renderer cache's second consumer: IngressOrientation tables rendered as VPP session
+ * rules for the VPP TCP host stack.
+ *   vpptcp.Renderer Init/NewTxn/Render/Commit  plugins/policy/renderer/vpptcp/vpptcp_renderer.go:58-188
+ *   dumpRules / updateRules                    vpptcp_renderer.go:191-316
+ *   rule.SessionRule, Export/ImportSessionRules plugins/policy/renderer/vpptcp/rule/session_rule.go:72-476
+ *   rule.IPv4Net (GetNsIndex/GetPodByAppNsIndex) session_rule.go:88-95      -> pg_appns
+ *   session_rule_add_del / session_rules_dump  binary API as mock/sessionrules/sessionrules_mock.go
+ *                                              holds it                    -> pg_session_rules
+ * Host-side control plane: the reference classifies nothing on this path (the session-rule
+ * lookup is VPP's). */
+enum { PG_SCOPE_GLOBAL = 1, PG_SCOPE_LOCAL = 2, PG_SCOPE_BOTH = 3 };
+#define PG_SR_ACTION_DO_NOTHING 0xFFFFFFFFu
+#define PG_SR_ACTION_DENY 0xFFFFFFFEu
+#define PG_SR_ACTION_ALLOW 0xFFFFFFFDu
+typedef struct pg_session_rule { /* rule.SessionRule (session_rule.go:73-86) */
+    uint8_t transport_proto;     /* 0 TCP, 1 UDP */
+    uint8_t is_ip4;
+    uint8_t lcl_ip[16];
+    uint8_t lcl_plen;
+    uint8_t rmt_ip[16];
+    uint8_t rmt_plen;
+    uint16_t lcl_port;
+    uint16_t rmt_port;
+    uint32_t action_index;
+    uint32_t appns_index;
+    uint8_t scope;
+    char tag[64];
+} pg_session_rule;
+typedef struct pg_session_rules pg_session_rules;
+typedef struct pg_appns pg_appns;
+typedef struct pg_vpptcp_renderer pg_vpptcp_renderer;
+typedef struct pg_vpptcp_txn pg_vpptcp_txn;
+
+/* VPP's session-rule tables; tag_prefix NULL = "contiv/vpp-policy" (rules with another tag
+ * are refused). Every add/del counts one request, a dump two (dump + control_ping). */
+pg_session_rules* pg_session_rules_new(const char* tag_prefix);
+void pg_session_rules_free(pg_session_rules* s);
+int pg_session_rules_clear(pg_session_rules* s);
+int pg_session_rules_counts(const pg_session_rules* s, int* req_count, int* err_count);
+/* session_rule_add_del: the reply's retval (0 ok, 1 refused: bad tag, duplicate add, unknown delete) */
+int pg_session_rule_add_del(pg_session_rules* s, const pg_session_rule* rule, int is_add);
+/* rules of the global table (scope GLOBAL) or of ns_index's local table (scope LOCAL), in
+ * installation order -> count (copies min(count, cap)) */
+int pg_session_rules_table(const pg_session_rules* s, int scope, uint32_t ns_index, pg_session_rule* out, size_t cap);
+/* MockSessionRules.{Local,Global}Table().HasRule: "" = unset address, a bare address = its
+ * one-host subnet; proto "TCP"/"UDP"; action "ALLOW"/"DENY" -> 1 / 0 */
+int pg_session_rules_has_rule(const pg_session_rules* s, int scope, uint32_t ns_index, const char* lcl_ip,
+                              uint16_t lcl_port, const char* rmt_ip, uint16_t rmt_port, const char* proto,
+                              const char* action);
+/* pod -> VPP application namespace index (IPv4Net.GetNsIndex / GetPodByAppNsIndex) */
+pg_appns* pg_appns_new(void);
+void pg_appns_free(pg_appns* a);
+int pg_appns_set(pg_appns* a, const char* pod_namespace, const char* pod_name, uint32_t ns_index);
+/* ExportSessionRules: pod_name NULL = global table -> count (copies min(count, cap)) */
+int pg_export_session_rules(const pg_appns* a, const pg_contiv_rule* rules, size_t n, const char* pod_namespace,
+                            const char* pod_name, const pg_ipnet* pod_ip, pg_session_rule* out, size_t cap);
+/* the renderer keeps pointers to vpp and ipv4net (both must outlive it); chan_buf_size =
+ * GoVPPChanBufSize (0 = 100: requests are sent in bursts of that size) */
+pg_vpptcp_renderer* pg_vpptcp_renderer_new(pg_session_rules* vpp, const pg_appns* ipv4net, int chan_buf_size);
+void pg_vpptcp_renderer_free(pg_vpptcp_renderer* r);
+const char* pg_vpptcp_last_error(const pg_vpptcp_renderer* r);
+pg_vpptcp_txn* pg_vpptcp_new_txn(pg_vpptcp_renderer* r, int resync);
+int pg_vpptcp_txn_render(pg_vpptcp_txn* t, const char* pod_namespace, const char* pod_name, const pg_ipnet* pod_ip,
+                         const pg_contiv_rule* ingress, size_t n_ingress, const pg_contiv_rule* egress,
+                         size_t n_egress, int removed);
+/* renders and programs the session rules, frees t; PG_EFAULT + pg_vpptcp_last_error when a
+ * request failed (the cache then keeps its previous state, as the reference's does) */
+int pg_vpptcp_txn_commit(pg_vpptcp_txn* t);
+void pg_vpptcp_txn_free(pg_vpptcp_txn* t);
+/* PolicyConfigurator.RegisterRenderer for the VPPTCP renderer */
+int pg_configurator_register_vpptcp(pg_configurator* c, pg_vpptcp_renderer* r);
+
 #ifdef __cplusplus
 }
 #endif

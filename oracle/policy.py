@@ -224,7 +224,8 @@ def compare_rule_lists(a, b) -> int:
 
 
 class ReferencePanic(RuntimeError):
-    """The reference would dereference a nil *ContivRule here (Go panic)."""
+    """The reference would dereference a nil pointer here (Go panic): a nil *ContivRule, or
+    the nil PodIP of a pod configuration rebuilt by a cache resync."""
 
 
 def compare_rules_to_padded(a, table) -> int:
@@ -337,8 +338,11 @@ def allowed_egress_ports(src_ip: IPNet, egress):
         if r.action == ACTION_DENY:
             has_deny = True
             continue
-        if not r.src.is_empty() and not gonet.contains(r.src, src_ip.ip):
-            continue
+        if not r.src.is_empty():
+            if src_ip is None:
+                raise ReferencePanic("nil pod IP in getAllowedEgressPorts")
+            if not gonet.contains(r.src, src_ip.ip):
+                continue
         if r.protocol == TCP:
             tcp.add(r.dst_port)
         elif r.protocol == UDP:
@@ -359,8 +363,11 @@ def allowed_ingress_ports(dst_ip: IPNet, ingress):
         if r.action == ACTION_DENY:
             has_deny = True
             continue
-        if not r.dst.is_empty() and not gonet.contains(r.dst, dst_ip.ip):
-            continue
+        if not r.dst.is_empty():
+            if dst_ip is None:
+                raise ReferencePanic("nil pod IP in getAllowedIngressPorts")
+            if not gonet.contains(r.dst, dst_ip.ip):
+                continue
         if r.protocol == TCP:
             tcp.add(r.dst_port)
         elif r.protocol == UDP:

@@ -99,6 +99,13 @@ class pg_policy(C.Structure):
                 ("n_matches", C.c_size_t)]
 
 
+class pg_session_rule(C.Structure):
+    _fields_ = [("transport_proto", C.c_uint8), ("is_ip4", C.c_uint8), ("lcl_ip", C.c_uint8 * 16),
+                ("lcl_plen", C.c_uint8), ("rmt_ip", C.c_uint8 * 16), ("rmt_plen", C.c_uint8),
+                ("lcl_port", C.c_uint16), ("rmt_port", C.c_uint16), ("action_index", C.c_uint32),
+                ("appns_index", C.c_uint32), ("scope", C.c_uint8), ("tag", C.c_char * 64)]
+
+
 _P = C.c_void_p
 _SIGS = {
     "pg_version": (C.c_char_p, []),
@@ -180,6 +187,28 @@ _SIGS = {
     "pg_gen_tuples": (C.c_int, [_P, C.POINTER(pg_gen_spec), C.c_uint64, _P, _P, _P, _P, _P, _P]),
     "pg_connections": (C.c_int, [_P, C.POINTER(pg_conn_query), C.c_size_t, C.POINTER(C.c_int32),
                                  C.POINTER(C.c_uint32)]),
+    "pg_session_rules_new": (_P, [C.c_char_p]),
+    "pg_session_rules_free": (None, [_P]),
+    "pg_session_rules_clear": (C.c_int, [_P]),
+    "pg_session_rules_counts": (C.c_int, [_P, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
+    "pg_session_rule_add_del": (C.c_int, [_P, C.POINTER(pg_session_rule), C.c_int]),
+    "pg_session_rules_table": (C.c_int, [_P, C.c_int, C.c_uint32, C.POINTER(pg_session_rule), C.c_size_t]),
+    "pg_session_rules_has_rule": (C.c_int, [_P, C.c_int, C.c_uint32, C.c_char_p, C.c_uint16, C.c_char_p,
+                                            C.c_uint16, C.c_char_p, C.c_char_p]),
+    "pg_appns_new": (_P, []),
+    "pg_appns_free": (None, [_P]),
+    "pg_appns_set": (C.c_int, [_P, C.c_char_p, C.c_char_p, C.c_uint32]),
+    "pg_export_session_rules": (C.c_int, [_P, C.POINTER(pg_contiv_rule), C.c_size_t, C.c_char_p, C.c_char_p,
+                                          C.POINTER(pg_ipnet), C.POINTER(pg_session_rule), C.c_size_t]),
+    "pg_vpptcp_renderer_new": (_P, [_P, _P, C.c_int]),
+    "pg_vpptcp_renderer_free": (None, [_P]),
+    "pg_vpptcp_last_error": (C.c_char_p, [_P]),
+    "pg_vpptcp_new_txn": (_P, [_P, C.c_int]),
+    "pg_vpptcp_txn_render": (C.c_int, [_P, C.c_char_p, C.c_char_p, C.POINTER(pg_ipnet), C.POINTER(pg_contiv_rule),
+                                       C.c_size_t, C.POINTER(pg_contiv_rule), C.c_size_t, C.c_int]),
+    "pg_vpptcp_txn_commit": (C.c_int, [_P]),
+    "pg_vpptcp_txn_free": (None, [_P]),
+    "pg_configurator_register_vpptcp": (C.c_int, [_P, _P]),
 }
 EXPORTED = sorted(_SIGS)
 

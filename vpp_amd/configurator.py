@@ -166,8 +166,11 @@ class PolicyConfigurator:
         assert lib.pg_configurator_set_nat_loopback(self.h, _b(ip) if ip else None) == 0
 
     def RegisterRenderer(self, r):
+        from . import vpptcp
         if isinstance(r, MockRenderer):
             rc = lib.pg_configurator_register_mock(self.h, r.h)
+        elif isinstance(r, vpptcp.Renderer):  # the VPPTCP session-rule renderer
+            rc = lib.pg_configurator_register_vpptcp(self.h, r.h)
         else:  # renderer.Renderer: the GPU ACL renderer
             rc = lib.pg_configurator_register_renderer(self.h, r.h)
         self._renderers.append(r)
