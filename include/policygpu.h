@@ -219,13 +219,19 @@ int pg_debug_walk_blob(pg_ctx* ctx, const char* acl_name, const uint32_t* src, c
  * same templates the kernels instantiate) run on the host over host tuples, any mode, with
  * optional host u64 counters. flags: bit 0 = node classifier when it exists (else the
  * per-table path), bit 1 = the predicated trie walks the kernels use on LDS-staged images
- * (else the branching ones they use on HBM-resident ones). Does not touch the device. */
+ * (else the branching ones they use on HBM-resident ones), bit 2 = the node image's
+ * common-row section when it was built (the kernels use it when it fits their LDS budget).
+ * Does not touch the device. */
 int pg_debug_classify_host(pg_ctx* ctx, int mode, int table_id, const pg_tuple_soa* tuples, uint64_t n,
                            uint32_t* out, uint64_t* counters, int flags);
 /* node classifier (PERPOD / CONN) size: IPv4 classes, L4-key classes, LDS image bytes,
  * cross-table bytes; PG_ENOENT when it was not built */
 int pg_node_stats(pg_ctx* ctx, uint32_t* ip_classes, uint32_t* key_classes, uint64_t* image_bytes,
                   uint64_t* cross_bytes);
+/* node image layout: bytes of the base image (without the common-row section), and how many of
+ * the covered (table, IPv4 class) pairs read the table's common row from the image instead of
+ * the cross table (0 when the section was not built); PG_ENOENT when there is no node */
+int pg_node_common_stats(pg_ctx* ctx, uint64_t* base_image_bytes, uint64_t* common_pairs, uint64_t* pairs);
 /* reference-shaped linear-scan kernel (K1) on one table, for validation and comparison */
 int pg_classify_linear(pg_ctx* ctx, int table_id, const pg_tuple_soa* tuples, uint64_t n, uint32_t* out,
                        void* hip_stream);

@@ -316,10 +316,11 @@ def test_k8s_object_cluster_gpu_vs_oracle(mode):
     assert len(np.unique(got >> 30)) >= 2
 
 
-def _classify_with(e, mode, b, node_path, stage_words=16384, counters=False):
+def _classify_with(e, mode, b, node_path, stage_words=16384, counters=False, common_lds=80 << 10):
     lib = R.lib
     assert lib.pg_set_tuning(b"node_path", node_path) == 0
     assert lib.pg_set_tuning(b"node_stage_max_words", stage_words) == 0
+    assert lib.pg_set_tuning(b"node_common_lds_max", common_lds) == 0
     try:
         out = torch.empty(b.n, dtype=torch.int32, device="cuda")
         cnt = torch.zeros(e.num_counter_slots(), dtype=torch.int64, device="cuda") if counters else None
@@ -329,6 +330,7 @@ def _classify_with(e, mode, b, node_path, stage_words=16384, counters=False):
     finally:
         lib.pg_set_tuning(b"node_path", 1)
         lib.pg_set_tuning(b"node_stage_max_words", 16384)
+        lib.pg_set_tuning(b"node_common_lds_max", 80 << 10)
 
 
 @pytest.mark.parametrize("config", [3, 5])
@@ -347,6 +349,12 @@ def test_node_kernel_equals_per_table_kernel(config):
     table, c3 = _classify_with(e, w.mode, b, 0, counters=True)
     assert np.array_equal(staged, hbm) and np.array_equal(staged, table)
     assert np.array_equal(c1, c2) and np.array_equal(c1, c3)
+    # the image's common-row section staged next to the histogram (STAGE 3), and left out
+    common, c4 = _classify_with(e, w.mode, b, 1, counters=True, common_lds=160 << 10)
+    base, c5 = _classify_with(e, w.mode, b, 1, counters=True, common_lds=0)
+    nocnt, _ = _classify_with(e, w.mode, b, 1)  # STAGE 3 at the default budget
+    assert np.array_equal(common, staged) and np.array_equal(base, staged) and np.array_equal(nocnt, staged)
+    assert np.array_equal(c4, c1) and np.array_equal(c5, c1)
     host = e.debug_classify_host(w.mode, -1, *b.numpy(b.n), node=True)
     assert np.array_equal(host, staged)
 

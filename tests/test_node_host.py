@@ -79,6 +79,13 @@ def check(e, local, tup, expect_node=True):
         assert np.array_equal(e.debug_classify_host(MODE_PERPOD, -1, *tup, node=node, pred=False), pn)
         assert np.array_equal(e.debug_classify_host(MODE_CONN, -1, *tup, node=node, pred=False),
                               e.debug_classify_host(MODE_CONN, -1, *tup, node=node))
+    # the node image without its common-row section (what the kernels run when it does not
+    # fit their LDS budget): same verdicts and counters
+    p0, c0 = e.debug_classify_host(MODE_PERPOD, -1, *tup, counters=True, node=True, common=False)
+    assert np.array_equal(p0, pn) and np.array_equal(c0, cpn)
+    q0, d0 = e.debug_classify_host(MODE_CONN, -1, *tup, counters=True, node=True, common=False)
+    q1, d1 = e.debug_classify_host(MODE_CONN, -1, *tup, counters=True, node=True)
+    assert np.array_equal(q0, q1) and np.array_equal(d0, d1)
     assert np.array_equal(pn, pt)
     assert np.array_equal(cpn, cpt)
     assert np.array_equal(pn >> 30, act.astype(np.uint32)), np.nonzero((pn >> 30) != act)[0][:8]
@@ -160,6 +167,8 @@ def test_config3_cluster_node_path():
     e = w.engine
     ns = e.node_stats()
     assert ns is not None and ns["image_bytes"] <= 64 << 10, ns  # staged in LDS by the kernel
+    # most (table, source class) rows are the table's common row (no rule admits the source)
+    assert ns["common_row_pairs"] >= 0.8 * ns["table_ipclass_pairs"], ns
     src, dst, sport, dport, proto = gen.gen_tuples(60001, **w.gen)
     wd = World(e, w.local_ifs, w.node_if)
     act, slot = wd.perpod(src, dst, dport, proto, threads=8)
@@ -168,3 +177,23 @@ def test_config3_cluster_node_path():
     conn, cslot = wd.conn(src, dst, sport, dport, proto, threads=8)
     got = e.debug_classify_host(MODE_CONN, -1, src, dst, sport, dport, proto, node=True)
     assert np.array_equal(got >> 30, conn.astype(np.uint32)) and np.array_equal(got & 0x3FFFFFFF, cslot)
+    got0 = e.debug_classify_host(MODE_CONN, -1, src, dst, sport, dport, proto, node=True, common=False)
+    assert np.array_equal(got0, got)
+
+
+def test_common_rows_disabled():
+    """node_common=0: the image has no common-row section and classifies the same."""
+    rnd = random.Random(77)
+    e, local, pod_ips = topology(rnd)
+    tup = tuples(78, 20000, pod_ips)
+    on = e.debug_classify_host(MODE_CONN, -1, *tup, node=True)
+    ns = e.node_stats()
+    assert ns["common_row_pairs"] > 0 and ns["image_bytes"] > ns["base_image_bytes"]
+    assert _capi.lib.pg_set_tuning(b"node_common", 0) == 0
+    try:
+        e2, local2, pod_ips2 = topology(random.Random(77))
+        ns2 = e2.node_stats()
+        assert ns2["common_row_pairs"] == 0 and ns2["image_bytes"] == ns2["base_image_bytes"]
+        assert np.array_equal(e2.debug_classify_host(MODE_CONN, -1, *tup, node=True), on)
+    finally:
+        assert _capi.lib.pg_set_tuning(b"node_common", 1) == 0

@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--tune", action="append", default=[], help="key=v1,v2,...")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=60, help="untimed launches before the first round")
     ap.add_argument("--counters", action="store_true", help="classify with per-rule hit counters")
     ap.add_argument("--pre", action="append", default=[], help="key=v set before the tables are compiled")
     ap.add_argument("--ns", type=int, default=0, help="configs 3/5: namespaces (default 10)")
@@ -56,6 +57,10 @@ def main():
     soa = b.soa()
     stream = C.c_void_p(torch.cuda.current_stream().cuda_stream)
     times = {i: [] for i in range(len(combos))}
+    # the first ~50 launches after the batch is generated run slower: warm up
+    for _ in range(a.warmup):
+        lib.pg_classify(e.h, w.mode, w.table_id, C.byref(soa), n, outs[0].data_ptr(), cptr, stream)
+    torch.cuda.synchronize()
     for r in range(a.rounds):
         for i, combo in enumerate(combos):
             for k, v in zip(keys, combo):

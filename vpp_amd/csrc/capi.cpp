@@ -163,6 +163,11 @@ int pg_set_tuning(const char* key, int value) {
         set_lc_lds((uint32_t)value);
         return PG_OK;
     }
+    if (std::string(key) == "node_common") {  // common-row section of node images compiled afterwards
+        if (value != 0 && value != 1) return PG_EINVAL;
+        set_node_common((uint32_t)value);
+        return PG_OK;
+    }
     if (std::string(key) == "node_build" || std::string(key) == "node_root_bits") {  // tables compiled afterwards
         static uint32_t enable = 1, bits = 12;
         if (std::string(key) == "node_build") {
@@ -532,7 +537,7 @@ DevTableSet host_view(const HostTableSet& h) {
     return v;
 }
 
-template <int MODE, int Q, bool PRED>
+template <int MODE, int Q, bool PRED, bool CM>
 void host_q(const DevTableSet& T, bool node, int table_id, const pg_tuple_soa* t, uint64_t i, uint32_t* out,
             const Hist& h) {
     uint32_t s[Q], d[Q], sp[Q], dp[Q], pr[Q], o[Q];
@@ -543,24 +548,26 @@ void host_q(const DevTableSet& T, bool node, int table_id, const pg_tuple_soa* t
     if constexpr (MODE == 0) {
         classify_q<0, true, Q, PRED>(T, T.blobs, load_tab(T.tabs, table_id), s, d, sp, dp, pr, h, o);
     } else {
-        if (node) classify_node_q<MODE, true, Q, PRED>(T, T.node, DevLoader{T.node.img}, s, d, sp, dp, pr, h, o);
+        if (node) classify_node_q<MODE, true, Q, PRED, CM>(T, T.node, DevLoader{T.node.img}, s, d, sp, dp, pr, h, o);
         else classify_q<MODE, true, Q, PRED>(T, T.blobs, DevTable{}, s, d, sp, dp, pr, h, o);
     }
     for (int j = 0; j < Q; j++) out[i + j] = o[j];
 }
 
-template <int MODE, bool PRED>
+template <int MODE, bool PRED, bool CM>
 void host_classify(const DevTableSet& T, bool node, int table_id, const pg_tuple_soa* t, uint64_t n, uint32_t* out,
                    const Hist& h) {
     const uint64_t nq = n & ~(uint64_t)3;  // the kernels' quads, then one tuple at a time
-    for (uint64_t i = 0; i < nq; i += 4) host_q<MODE, 4, PRED>(T, node, table_id, t, i, out, h);
-    for (uint64_t i = nq; i < n; i++) host_q<MODE, 1, PRED>(T, node, table_id, t, i, out, h);
+    for (uint64_t i = 0; i < nq; i += 4) host_q<MODE, 4, PRED, CM>(T, node, table_id, t, i, out, h);
+    for (uint64_t i = nq; i < n; i++) host_q<MODE, 1, PRED, CM>(T, node, table_id, t, i, out, h);
 }
 template <int MODE>
-void host_classify(const DevTableSet& T, bool node, bool pred, int table_id, const pg_tuple_soa* t, uint64_t n,
-                   uint32_t* out, const Hist& h) {
-    if (pred) host_classify<MODE, true>(T, node, table_id, t, n, out, h);
-    else host_classify<MODE, false>(T, node, table_id, t, n, out, h);
+void host_classify(const DevTableSet& T, bool node, bool pred, bool cm, int table_id, const pg_tuple_soa* t,
+                   uint64_t n, uint32_t* out, const Hist& h) {
+    if (pred && cm) host_classify<MODE, true, true>(T, node, table_id, t, n, out, h);
+    else if (pred) host_classify<MODE, true, false>(T, node, table_id, t, n, out, h);
+    else if (cm) host_classify<MODE, false, true>(T, node, table_id, t, n, out, h);
+    else host_classify<MODE, false, false>(T, node, table_id, t, n, out, h);
 }
 }  // namespace
 
@@ -579,10 +586,11 @@ int pg_debug_classify_host(pg_ctx* ctx, int mode, int table_id, const pg_tuple_s
     if (!out || !t->src_ip || !t->dst_ip || !t->dst_port || !t->proto || (mode == PG_MODE_CONN && !t->src_port))
         return fail(ctx, PG_EINVAL, "missing tuple field");
     const bool use_node = (node & 1) && T.node.img != nullptr, pred = (node & 2) != 0;
+    const bool cm = use_node && (node & 4) && T.node.cmap != 0;
     const Hist h{nullptr, (unsigned long long*)counters};
-    if (mode == 0) host_classify<0>(T, false, pred, table_id, t, n, out, h);
-    else if (mode == 1) host_classify<1>(T, use_node, pred, table_id, t, n, out, h);
-    else host_classify<2>(T, use_node, pred, table_id, t, n, out, h);
+    if (mode == 0) host_classify<0>(T, false, pred, false, table_id, t, n, out, h);
+    else if (mode == 1) host_classify<1>(T, use_node, pred, cm, table_id, t, n, out, h);
+    else host_classify<2>(T, use_node, pred, cm, table_id, t, n, out, h);
     return PG_OK;
     GUARD_END(ctx)
 }
@@ -599,6 +607,25 @@ int pg_node_stats(pg_ctx* ctx, uint32_t* ip_classes, uint32_t* key_classes, uint
     if (key_classes) *key_classes = h.node.gk;
     if (image_bytes) *image_bytes = h.node_img.size() * 4;
     if (cross_bytes) *cross_bytes = h.node_cross.size() * 4;
+    return PG_OK;
+    GUARD_END(ctx)
+}
+
+int pg_node_common_stats(pg_ctx* ctx, uint64_t* base_image_bytes, uint64_t* common_pairs, uint64_t* pairs) {
+    if (!ctx) return PG_EINVAL;
+    GUARD_BEGIN
+    Engine& E = ctx->eng;
+    if (!E.compiled) E.compile();
+    const HostTableSet& h = E.host;
+    if (h.node_img.empty()) return fail(ctx, PG_ENOENT, "no node classifier (disabled or over budget)");
+    uint64_t covered = 0, common = 0;
+    for (size_t t = 0; t < h.tabs.size(); t++)
+        if (h.node_img[h.node.tabinfo + 4 * t + 1] >> 31) covered++;
+    if (h.node.cmap)
+        for (size_t i = h.node.cmap; i < h.node.img_words; i++) common += (uint64_t)__builtin_popcount(h.node_img[i]);
+    if (base_image_bytes) *base_image_bytes = (uint64_t)h.node.img_words_base * 4;
+    if (common_pairs) *common_pairs = common;
+    if (pairs) *pairs = covered * h.node.n_ipc;
     return PG_OK;
     GUARD_END(ctx)
 }

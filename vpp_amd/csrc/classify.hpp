@@ -24,6 +24,9 @@ namespace pg {
 #else
 #define PG_NOINLINE inline
 #endif
+#ifndef PG_AGG_ROUNDS  // wave-aggregation rounds of hit-counter increments (Hist::inc)
+#define PG_AGG_ROUNDS 0
+#endif
 #ifndef PG_NODE_FB_Q1  // node kernels: per-table fallback one tuple at a time
 #define PG_NODE_FB_Q1 1
 #endif
@@ -166,12 +169,13 @@ struct Hist {
     unsigned long long* glob;
     PG_HD void inc(uint32_t slot) const {
 #if defined(__HIP_DEVICE_COMPILE__)
-        // A few slots take most hits (a reflective ACL's rule, "no ACL", a default deny):
-        // twice, the lanes sharing the first active lane's slot add their count with one
-        // atomic; the rest add one each.
+        // One LDS (or global) atomic per lane. PG_AGG_ROUNDS > 0 first lets the lanes that
+        // share the first active lane's slot (a reflective ACL's rule, "no ACL", a default
+        // deny) add their count with one atomic, per round; A/B on MI355X with warmed-up
+        // launches (tools/sweep.py): 0 rounds beats 1 / 2 / 3 by 3-14 % on configs 2, 3, 5.
         bool done = false;
 #pragma unroll
-        for (int r = 0; r < 2; r++) {
+        for (int r = 0; r < PG_AGG_ROUNDS; r++) {
             if (!done) {
                 const uint32_t lead = __builtin_amdgcn_readfirstlane(slot);
                 const unsigned long long m = __ballot(slot == lead);
@@ -267,7 +271,9 @@ struct NoHook {
 
 // H: called once per lane, right after the first evaluation's cross-entry loads are issued
 // (the kernels issue the next quad's stream loads there; see device.hip PG_PREFETCH)
-template <class L, int Q, class H = NoHook>
+// CM: the node image's common-row section is in use (device.hpp DevNode): evaluations whose
+// (table, IP class) row is the table's common row read it from the image, not the cross table.
+template <class L, int Q, class H = NoHook, bool CM = false>
 struct NodeEval {
     const DevTableSet& T;
     const DevNode& N;
@@ -289,17 +295,25 @@ struct NodeEval {
         const uint32_t(&k)[Q] = rev ? kack : ksyn;
         const uint32_t(&ca)[Q] = rev ? cd : cs;
         const uint32_t(&gk)[Q] = rev ? gack : gsyn;
-        bool on[Q], fb[Q], pend[Q];
+        bool on[Q], fb[Q], pend[Q], cm[Q];
         uint32_t pos[Q];
         PG_UNROLL
         for (int j = 0; j < Q; j++) {
-            on[j] = false;
+            on[j] = cm[j] = false;
+            pos[j] = 0;
             if (act[j] && k[j] < kWalkKeyLimit) {
-                const W2 ti = img.u2(N.tabinfo + 2u * (uint32_t)t[j]);  // {cross base, nkc | covered << 31}
+                // {cross base, nkc | covered << 31, common row, 0}
+                const W4 ti = img.u4(N.tabinfo + 4u * (uint32_t)t[j]);
                 if (ti.y >> 31) {
                     const uint32_t ki = (uint32_t)t[j] * N.gk + gk[j];
+                    uint32_t cw = 0;
+                    if (CM) {
+                        const uint32_t b = (uint32_t)t[j] * N.n_ipc + ca[j];
+                        cw = img.u32(N.cmap + (b >> 5u)) >> (b & 31u);
+                    }
                     const uint32_t lk = (img.u32(N.kmap + (ki >> 1)) >> ((ki & 1u) * 16u)) & 0xFFFFu;
-                    pos[j] = ti.x + ca[j] * (ti.y & 0xFFFFu) + lk;
+                    cm[j] = CM && (cw & 1u);
+                    pos[j] = cm[j] ? ti.z + lk : ti.x + ca[j] * (ti.y & 0xFFFFu) + lk;
                     on[j] = true;
                 }
             }
@@ -312,8 +326,13 @@ struct NodeEval {
 #if defined(PG_PROBE_NOGATHER)  // measurement build only: no cross-entry load
             w[j] = pos[j] & 0x3FFFu;
 #else
-            w[j] = X.u32(pos[j]);
+            if (!cm[j]) w[j] = X.u32(pos[j]);
 #endif
+        }
+        if (CM) {
+            PG_UNROLL
+            for (int j = 0; j < Q; j++)
+                if (on[j] && cm[j]) w[j] = img.u32(pos[j]);
         }
         if (!*hooked) {
             *hooked = true;
@@ -527,7 +546,7 @@ PG_HD void classify_q(const DevTableSet& T, const uint32_t* blobs, const DevTabl
 
 // Q tuples of one lane, PERPOD / CONN, node path. `img` reads the node image (LDS copy or
 // global memory).
-template <int MODE, bool COUNT, int Q, bool PRED = false, class L, class H = NoHook>
+template <int MODE, bool COUNT, int Q, bool PRED = false, bool CM = false, class L, class H = NoHook>
 PG_HD void classify_node_q(const DevTableSet& T, const DevNode& N, const L& img, const uint32_t (&s)[Q],
                            const uint32_t (&d)[Q], const uint32_t (&sp)[Q], const uint32_t (&dp)[Q],
                            const uint32_t (&pr)[Q], const Hist& h, uint32_t (&out)[Q], const H& hook = H()) {
@@ -566,7 +585,7 @@ PG_HD void classify_node_q(const DevTableSet& T, const DevNode& N, const L& img,
     PG_UNROLL
     for (int j = 0; j < Q; j++) cs[j] = ipc[j], cd[j] = ipc[Q + j];
     bool hooked = false;
-    const NodeEval<L, Q, H> ev{T, N, img, s, d, key, kack, cs, cd, gs, ga, hook, &hooked};
+    const NodeEval<L, Q, H, CM> ev{T, N, img, s, d, key, kack, cs, cd, gs, ga, hook, &hooked};
     if (MODE == 1) {
         int32_t t[Q];
         bool run[Q];

@@ -330,9 +330,9 @@ __global__ __launch_bounds__(BS) void k_classify(DevTableSet T, int32_t t, const
                 cs[j] = sv[c + j], cd[j] = dv[c + j], csp[j] = spv[c + j], cdp[j] = dpv[c + j], cpr[j] = prv[c + j];
             if constexpr (NODE) {
                 if (c == 0)
-                    classify_node_q<MODE, COUNT, QC, STAGE && PG_PRED>(T, T.node, img, cs, cd, csp, cdp, cpr, h, co, hook);
+                    classify_node_q<MODE, COUNT, QC, STAGE && PG_PRED, STAGE == 3>(T, T.node, img, cs, cd, csp, cdp, cpr, h, co, hook);
                 else
-                    classify_node_q<MODE, COUNT, QC, STAGE && PG_PRED>(T, T.node, img, cs, cd, csp, cdp, cpr, h, co);
+                    classify_node_q<MODE, COUNT, QC, STAGE && PG_PRED, STAGE == 3>(T, T.node, img, cs, cd, csp, cdp, cpr, h, co);
             } else {
                 classify_q<MODE, COUNT, QC, STAGE == 1 && PG_PRED>(T, blobs, tab0, cs, cd, csp, cdp, cpr, h, co, rootb);
             }
@@ -352,7 +352,7 @@ __global__ __launch_bounds__(BS) void k_classify(DevTableSet T, int32_t t, const
         const uint32_t s1[1] = {src[i]}, d1[1] = {dst[i]}, sp1[1] = {MODE == 2 ? (uint32_t)sport[i] : 0u},
                        dp1[1] = {dport[i]}, pr1[1] = {proto[i]};
         uint32_t o[1];
-        if constexpr (NODE) classify_node_q<MODE, COUNT, 1, STAGE && PG_PRED>(T, T.node, img, s1, d1, sp1, dp1, pr1, h, o);
+        if constexpr (NODE) classify_node_q<MODE, COUNT, 1, STAGE && PG_PRED, STAGE == 3>(T, T.node, img, s1, d1, sp1, dp1, pr1, h, o);
         else classify_q<MODE, COUNT, 1, STAGE == 1 && PG_PRED>(T, blobs, tab0, s1, d1, sp1, dp1, pr1, h, o, rootb);
         out[i] = o[0];
     }
@@ -492,8 +492,12 @@ static uint32_t g_stage_max_words = kStageBlobWords;  // blobs up to 64 KiB are 
 static uint32_t g_node_stage_max_words = 16384;  // node images up to 64 KiB are staged in LDS
 static uint32_t g_stage_root_max_words = 16400;  // larger blobs: header + src root up to 2^14 entries
 static uint32_t g_node_path = 1;            // PERPOD / CONN through the node classifier when built
-// workgroup size of LDS-staged classify launches; 0 = per mode (SINGLE 1024, PERPOD / CONN
-// 512: tools/sweep.py on MI355X)
+// LDS bytes (image + counter histogram) up to which a node image's common-row section is staged
+// and used: 80 KiB keeps two 512-thread workgroups per CU
+static size_t g_node_common_lds_max = 80u << 10;
+constexpr uint32_t kCommonStageExtraWords = 8192;  // the section may take the image past the base cap
+// workgroup size of LDS-staged classify launches; 0 = per mode (SINGLE 1024, SINGLE with
+// counters and PERPOD / CONN 512: tools/sweep.py on MI355X)
 static uint32_t g_block_stage = 0;
 
 int dev_set_tuning(const std::string& key, int value) {
@@ -502,6 +506,7 @@ int dev_set_tuning(const std::string& key, int value) {
     else if (key == "node_stage_max_words" && value >= 0 && value <= 36864) g_node_stage_max_words = (uint32_t)value;
     else if (key == "stage_root_max_words" && value >= 0 && value <= 36864) g_stage_root_max_words = (uint32_t)value;
     else if (key == "node_path" && (value == 0 || value == 1)) g_node_path = (uint32_t)value;
+    else if (key == "node_common_lds_max" && value >= 0 && value <= (160 << 10)) g_node_common_lds_max = (size_t)value;
     else if (key == "block_stage" && (value == 0 || value == 256 || value == 512 || value == 1024))
         g_block_stage = (uint32_t)value;
     else return -1;
@@ -556,7 +561,9 @@ static void launch_one(const DevTableSet& T, int t, const uint32_t* src, const u
                        const uint16_t* dport, const uint8_t* proto, uint64_t n, uint32_t* out,
                        unsigned long long* counters, hipStream_t st, size_t hist, uint32_t stage, uint64_t items) {
     if constexpr (STAGE) {
-        const uint32_t bs = g_block_stage ? g_block_stage : (MODE == 0 ? 1024u : 512u);
+        // SINGLE with counters: 512 (A/B on MI355X: +14 % at config 2 with counters, the
+        // same without)
+        const uint32_t bs = g_block_stage ? g_block_stage : (MODE == 0 && !COUNT ? 1024u : 512u);
         if (bs == 1024u)
             return launch_bs<MODE, COUNT, VEC, STAGE, NODE, 1024>(T, t, src, dst, sport, dport, proto, n, out, counters,
                                                                   st, hist, stage, items);
@@ -588,9 +595,15 @@ static void launch_classify(const DevTableSet& T, int t, const uint32_t* src, co
             launch_one<MODE, COUNT, VEC, 0, false>(T, t, src, dst, sport, dport, proto, n, out, counters, st, hist,
                                                    0, items);
     } else if (g_node_path && T.node.img) {
-        if (T.node.img_words <= g_node_stage_max_words)
-            launch_one<MODE, COUNT, VEC, 1, true>(T, t, src, dst, sport, dport, proto, n, out, counters, st, hist,
+        // the image with its common-row section when that fits the LDS budget next to the
+        // histogram, else the base image (STAGE 1), else the image is read from HBM / L2
+        if (T.node.cmap && hist + (size_t)T.node.img_words * 4 <= g_node_common_lds_max &&
+            T.node.img_words <= g_node_stage_max_words + kCommonStageExtraWords)
+            launch_one<MODE, COUNT, VEC, 3, true>(T, t, src, dst, sport, dport, proto, n, out, counters, st, hist,
                                                   T.node.img_words, items);
+        else if (T.node.img_words_base <= g_node_stage_max_words)
+            launch_one<MODE, COUNT, VEC, 1, true>(T, t, src, dst, sport, dport, proto, n, out, counters, st, hist,
+                                                  T.node.img_words_base, items);
         else
             launch_one<MODE, COUNT, VEC, 0, true>(T, t, src, dst, sport, dport, proto, n, out, counters, st, hist,
                                                   0, items);

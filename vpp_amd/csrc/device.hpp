@@ -45,14 +45,21 @@ struct DevTable {          // 32 B: two 16-B loads
 // cross-table entry per evaluation.
 //   img    u32[]  IPv4 trie (root at word 0, leaf = node IP class) | L4-key trie (leaf = node
 //                 key class) | ipinfo uint2[n_ipc] {interface, tin | tout << 16} | tabinfo
-//                 uint2[T] {cross base, nkc | covered << 31} | kmap u16[T][gk] (local key class)
+//                 uint4[T] {cross base, nkc | covered << 31, common row, 0} | kmap u16[T][gk]
+//                 (local key class) | the words up to img_words_base are the base image;
+//                 then the common-row section (cmap != 0): per covered table its most
+//                 frequent cross row (u32[nkc], at tabinfo.z) and a bitmap over [T][n_ipc],
+//                 bit set = that (table, ip class) row equals the table's common row, so the
+//                 entry is read from the (LDS-staged) image instead of the cross table
 //   cross  u32[]  per covered table, [ip class][local key class] -> verdict, or kNodeList |
 //                 first dst record (16 B records, blobwalk.hpp, ending with a match-all one)
 constexpr uint32_t kNodeList = 1u << 29, kNodeRecMask = kNodeList - 1u;
 struct DevNode {
     const uint32_t* img;   // null: no node classifier (the per-table path runs)
     const uint32_t* cross;
-    uint32_t img_words;
+    uint32_t img_words;    // whole image (with the common-row section when cmap != 0)
+    uint32_t img_words_base;  // image without the common-row section
+    uint32_t cmap;         // word offset of the common-row bitmap in img, 0 = none
     uint32_t ip_s1, key_root, key_k1;
     uint32_t ipinfo, tabinfo, kmap;  // word offsets in img
     uint32_t gk;           // node key classes
@@ -115,6 +122,7 @@ bool build_node(HostTableSet& h, const std::vector<TableAnalysis*>& an, const st
                 const NodePod& node_end);
 void set_root_bits_max(uint32_t bits);  // cap of the tries' root stride (4..16)
 void set_node_tuning(uint32_t enable, uint32_t root_bits);
+void set_node_common(uint32_t on);  // common-row section of the node image (images compiled afterwards)
 void set_pair_enable(uint32_t on);  // PAIR mode for tables CROSS cannot take (tables compiled afterwards)
 void set_lc_node(uint32_t on);  // level-compressed node IPv4 trie (tables compiled afterwards)
 void set_lc_lds(uint32_t on);

@@ -134,6 +134,7 @@ uint32_t g_pair_enable = 1;  // PAIR mode for tables CROSS cannot take (else CAN
 constexpr uint32_t kPairMaxRules = 1u << 16;
 constexpr uint64_t kPairBudget = 1ull << 22;  // entries of each PAIR phase table (16 MiB)
 constexpr size_t kPairListMin = 16;  // CROSS dst lists longer than this: PAIR instead
+uint32_t g_node_common = 1;               // common-row section of the node image
 uint32_t g_node_root_bits = 12;           // node IPv4 trie root: 2^12 words = 16 KiB
 constexpr uint64_t kNodeCrossBudget = 1ull << 25;  // node cross entries (128 MiB)
 
@@ -159,6 +160,7 @@ void set_root_bits_max(uint32_t bits) { g_root_bits_max = std::max<uint32_t>(4, 
 void set_lc_node(uint32_t on) { g_lc_node = on; }
 void set_pair_enable(uint32_t on) { g_pair_enable = on; }
 void set_lc_dense12(uint32_t n) { g_lc_dense12 = n; }
+void set_node_common(uint32_t on) { g_node_common = on; }
 void set_node_tuning(uint32_t enable, uint32_t root_bits) {
     g_node_enable = enable;
     g_node_root_bits = std::max<uint32_t>(4, std::min<uint32_t>(16, root_bits));
@@ -536,6 +538,56 @@ bool build_fast_table(const DevRule* rules, uint32_t n, uint32_t rule_base, uint
 // Then cross[t][ip class][local key class] is table t's cross entry for (its src class of
 // that IP class, key class): an evaluation is two LDS trie walks (shared by every table and
 // both directions of a connection) and one global load.
+// Common-row section of the node image (device.hpp DevNode): per covered table, the cross row
+// (over its key classes) shared by the most node IP classes -- typically "no rule admits this
+// source": the default deny -- and a bitmap of the (table, IP class) pairs whose row equals it.
+// Those evaluations read their entry from the LDS-staged image instead of gathering it from
+// the cross table. Appended after the base image; the kernels stage and use it when the LDS
+// budget allows (device.hip). Skipped when the bitmap would exceed kCommonMapMaxBits.
+constexpr uint64_t kCommonMapMaxBits = 1ull << 20;  // 128 KiB
+void build_common_rows(HostTableSet& h, const std::vector<uint32_t>& cov, const std::vector<TableAnalysis*>& an) {
+    std::vector<uint32_t>& img = h.node_img;
+    DevNode& N = h.node;
+    const uint32_t T = (uint32_t)h.tabs.size(), G = N.n_ipc;
+    const uint64_t bits = (uint64_t)T * G;
+    if (!g_node_common || bits > kCommonMapMaxBits) return;
+    const std::vector<uint32_t>& X = h.node_cross;
+    std::vector<uint32_t> sec, map((size_t)((bits + 31) / 32), 0);
+    std::vector<uint32_t> crow(T, 0);
+    for (uint32_t t : cov) {
+        const uint32_t base = img[N.tabinfo + 4 * t], nk = an[t]->nkc;
+        // most frequent row: rows hashed, candidates compared word by word
+        std::unordered_map<uint64_t, std::pair<uint32_t, uint32_t>> freq;  // hash -> (first ip class, count)
+        auto row = [&](uint32_t g) { return X.data() + base + (size_t)g * nk; };
+        auto hrow = [&](uint32_t g) {
+            uint64_t x = 1469598103934665603ull;
+            for (uint32_t k = 0; k < nk; k++) x = (x ^ row(g)[k]) * 1099511628211ull;
+            return x;
+        };
+        uint32_t best = 0, best_n = 0;
+        for (uint32_t g = 0; g < G; g++) {
+            auto& f = freq.emplace(hrow(g), std::make_pair(g, 0u)).first->second;
+            if (!std::equal(row(g), row(g) + nk, row(f.first))) continue;  // hash collision: not counted
+            if (++f.second > best_n) best_n = f.second, best = f.first;
+        }
+        crow[t] = (uint32_t)sec.size();
+        sec.insert(sec.end(), row(best), row(best) + nk);
+        for (uint32_t g = 0; g < G; g++)
+            if (std::equal(row(g), row(g) + nk, row(best))) {
+                const uint64_t b = (uint64_t)t * G + g;
+                map[b >> 5] |= 1u << (b & 31u);
+            }
+    }
+    while (sec.size() % 4) sec.push_back(0);
+    const uint32_t s0 = (uint32_t)img.size();
+    for (uint32_t t : cov) img[N.tabinfo + 4 * t + 2] = s0 + crow[t];
+    img.insert(img.end(), sec.begin(), sec.end());
+    N.cmap = (uint32_t)img.size();
+    img.insert(img.end(), map.begin(), map.end());
+    while (img.size() % 4) img.push_back(0);
+    N.img_words = (uint32_t)img.size();
+}
+
 bool build_node(HostTableSet& h, const std::vector<TableAnalysis*>& an, const std::vector<NodePod>& pods,
                 const NodePod& node_end) {
     h.node_img.clear();
@@ -632,14 +684,16 @@ bool build_node(HostTableSet& h, const std::vector<TableAnalysis*>& an, const st
         img.push_back(k[0]);
         img.push_back(t16(k[1]) | (t16(k[2]) << 16));
     }
+    while (img.size() % 4) img.push_back(0);
     N.tabinfo = (uint32_t)img.size();
-    img.resize(img.size() + 2 * (size_t)T, 0);
+    img.resize(img.size() + 4 * (size_t)T, 0);
     N.kmap = (uint32_t)img.size();
     img.resize(img.size() + ((size_t)T * GK + 1) / 2, 0);
     while (img.size() % 4) img.push_back(0);
     N.gk = GK;
     N.n_ipc = G;
-    N.img_words = (uint32_t)img.size();
+    N.img_words = N.img_words_base = (uint32_t)img.size();
+    N.cmap = 0;
 
     // cross entries, then the dst records of the pairs with a list
     std::vector<uint32_t>& X = h.node_cross;
@@ -649,8 +703,8 @@ bool build_node(HostTableSet& h, const std::vector<TableAnalysis*>& an, const st
     for (size_t c = 0; c < C; c++) {
         const uint32_t t = cov[c];
         const TableAnalysis& A = *an[t];
-        img[N.tabinfo + 2 * t] = (uint32_t)X.size();
-        img[N.tabinfo + 2 * t + 1] = A.nkc | 0x80000000u;
+        img[N.tabinfo + 4 * t] = (uint32_t)X.size();
+        img[N.tabinfo + 4 * t + 1] = A.nkc | 0x80000000u;
         for (uint32_t g = 0; g < GK; g++) {
             const uint32_t ki = t * GK + g;
             img[N.kmap + ki / 2] |= kc_key[g][c] << ((ki & 1u) * 16u);
@@ -684,6 +738,7 @@ bool build_node(HostTableSet& h, const std::vector<TableAnalysis*>& an, const st
             }
         }
     }
+    build_common_rows(h, cov, an);
     X.resize(rec0, 0);
     X.insert(X.end(), recs.begin(), recs.end());
     if (X.empty()) X.resize(4, 0);

@@ -255,8 +255,9 @@ class Engine:
         return out
 
     def debug_classify_host(self, mode, table_id, src, dst, sport, dport, proto, counters=False, node=True,
-                            pred=True):
+                            pred=True, common=True):
         """TESTS ONLY: pg_classify's per-tuple code run on the host (pg_debug_classify_host).
+        ``common``: the node image's common-row section (when it was built).
         -> verdict words (u32), and the u64 hit counters when ``counters``."""
         import numpy as np
         n = len(src)
@@ -268,7 +269,7 @@ class Engine:
         cnt = np.zeros(self.num_counter_slots(), np.uint64) if counters else None
         self._ck(lib.pg_debug_classify_host(self.h, mode, table_id, C.byref(t), n, p(out),
                                             p(cnt) if counters else None,
-                                            int(node) | (2 if pred else 0)))
+                                            int(node) | (2 if pred else 0) | (4 if common else 0)))
         return (out, cnt) if counters else out
 
     def node_stats(self):
@@ -279,7 +280,11 @@ class Engine:
         if rc == -2:  # PG_ENOENT
             return None
         self._ck(rc)
-        return {"ip_classes": a.value, "key_classes": b.value, "image_bytes": c.value, "cross_bytes": d.value}
+        st = {"ip_classes": a.value, "key_classes": b.value, "image_bytes": c.value, "cross_bytes": d.value}
+        base, common, pairs = C.c_uint64(), C.c_uint64(), C.c_uint64()
+        self._ck(lib.pg_node_common_stats(self.h, C.byref(base), C.byref(common), C.byref(pairs)))
+        st.update(base_image_bytes=base.value, common_row_pairs=common.value, table_ipclass_pairs=pairs.value)
+        return st
 
     def slot_of_rule(self, tid, idx):
         """counter slot of rule ``idx`` of table ``tid`` (idx -1: the table's default deny)."""
