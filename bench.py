@@ -42,7 +42,9 @@ def parse():
     p.add_argument("--config", type=int, default=2, choices=sorted(W.CONFIGS))
     p.add_argument("--tuples", type=int, default=0, help="tuples per GPU (default: the config's)")
     p.add_argument("--counters", action="store_true", help="time with per-rule hit counters on")
-    p.add_argument("--cpu-sample", type=int, default=4 << 20, help="tuples in the CPU-baseline sample")
+    p.add_argument("--cpu-sample", type=int, default=16 << 20, help="tuples in the CPU-baseline sample")
+    p.add_argument("--faithful-seconds", type=float, default=8.0,
+                   help="budget of the single-thread reference-faithful CPU variant (SINGLE mode)")
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--per-table", action="store_true",
                    help="PERPOD/CONN through the per-table blobs + IP hash instead of the node classifier")
@@ -129,7 +131,7 @@ def main():
     if allreduce_ms is not None:
         line["counter_allreduce_ms"] = round(allreduce_ms, 3)
     if rank == 0 and world == 1 and not a.no_cpu:
-        line["cpu_baseline"], line["parity_sample"] = cpu_baseline(w, b, out, a.cpu_sample)
+        line["cpu_baseline"], line["parity_sample"] = cpu_baseline(w, b, out, a.cpu_sample, a.faithful_seconds)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:
@@ -160,7 +162,7 @@ def pmc_traffic(config, n, counters):
     return int(p["hbm_traffic_bytes_per_launch"] * n / p["tuples_per_launch"]), os.path.basename(files[-1])
 
 
-def cpu_baseline(w, b, out, k):
+def cpu_baseline(w, b, out, k, faithful_s=8.0):
     """The oracle's evalACL/testConnection (oracle/oracle.c) timed on this host's cores over
     the first k tuples of the same workload; also checks the GPU verdicts on that sample."""
     from oracle import fast, world  # cpu_baseline leg: the checker, never the thing measured on GPU
@@ -171,6 +173,7 @@ def cpu_baseline(w, b, out, k):
     e = w.engine
     threads = min(16, os.cpu_count() or 1)
     extra = {}
+    faithful_ok = None
     if w.mode == 0:
         ora = fast.OraACL(e.GetACLByName(e.ACLNames()[w.table_id])["rules"])
         t0 = time.perf_counter()
@@ -180,12 +183,19 @@ def cpu_baseline(w, b, out, k):
         dflt = e.slot_of_rule(w.table_id, -1)
         slot = np.where(idx >= 0, base + idx.astype(np.int64), dflt).astype(np.uint32)
         kind = "evalACL over the same ACL (rules pre-parsed), %d threads" % threads
-        # reference-faithful variant (CIDR strings parsed per rule visit, one thread), small sample
-        kf = min(k, 1 << 16)
+        # reference-faithful variant (CIDR strings parsed per rule visit, one thread): a
+        # 4096-tuple calibration run sizes the sample to about faithful_s seconds
         rules = e.GetACLByName(e.ACLNames()[w.table_id])["rules"]
         t0 = time.perf_counter()
-        fast.eval_acl_faithful(rules, src[:kf], dst[:kf], dport[:kf], proto[:kf])
+        fast.eval_acl_faithful(rules, src[:4096], dst[:4096], dport[:4096], proto[:4096])
+        rate = 4096 / max(time.perf_counter() - t0, 1e-9)
+        kf = int(min(k, max(4096, rate * faithful_s)))
+        t0 = time.perf_counter()
+        fa, fi = fast.eval_acl_faithful(rules, src[:kf], dst[:kf], dport[:kf], proto[:kf])
         extra["faithful_1thread_mpps"] = round(kf / (time.perf_counter() - t0) / 1e6, 4)
+        extra["faithful_sample"] = kf
+        fslot = np.where(fi >= 0, base + fi.astype(np.int64), dflt).astype(np.uint32)
+        faithful_ok = bool(((got[:kf] >> 30) == fa.astype(np.uint32)).all() and ((got[:kf] & 0x3FFFFFFF) == fslot).all())
     else:
         wd = world.World(e, w.local_ifs, w.node_if)
         sif, dif = wd.resolve(src), wd.resolve(dst)  # interface lookup kept outside the timed call
@@ -204,7 +214,10 @@ def cpu_baseline(w, b, out, k):
     base = {"value": round(k / dt / 1e6, 3), "unit": "Mpps", "cores": threads, "kind": "port",
             "sample": "first %d tuples of the same workload; %s" % (k, kind)}
     base.update(extra)
-    return base, {"tuples": k, "bit_exact_action_and_rule_index": ok}
+    parity = {"tuples": k, "bit_exact_action_and_rule_index": ok}
+    if faithful_ok is not None:
+        parity["faithful_variant_bit_exact"] = faithful_ok
+    return base, parity
 
 
 if __name__ == "__main__":
