@@ -26,6 +26,24 @@ constexpr uint32_t kLeaf = 0x80000000u;
 constexpr uint32_t kTrieStrideShift = 26u, kTrieChildMask = (1u << kTrieStrideShift) - 1u;
 PG_HD uint32_t trie_child(uint32_t e) { return e & kTrieChildMask; }
 PG_HD uint32_t trie_stride(uint32_t e) { return (e >> kTrieStrideShift) & 31u; }
+// Node-image tries (LDS-staged): non-leaf entry = child byte offset << 10 | stride << 5 | shift
+// of the child level. The child entry of address a is at byte
+//   (e >> 10) + 4 * ((a >> (e & 31)) & ((1 << ((e >> 5) & 31)) - 1))
+// -- on the device one v_bfe_u32 (it reads only the low 5 bits of its offset and width
+// operands) and one v_lshl_add_u32.
+constexpr uint32_t kNodeChildMaxWords = 1u << 19;  // 2 MiB of image
+PG_HD constexpr uint32_t node_entry(uint32_t child_words, uint32_t stride, uint32_t shift) {
+    return (child_words * 4u) << 10 | stride << 5 | shift;
+}
+PG_HD uint32_t node_child_byte(uint32_t e, uint32_t a) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const uint32_t idx = __builtin_amdgcn_ubfe(a, e, e >> 5);
+#else
+    const uint32_t w = (e >> 5) & 31u;
+    const uint32_t idx = (a >> (e & 31u)) & ((1u << w) - 1u);
+#endif
+    return (e >> 10) + (idx << 2);
+}
 constexpr uint32_t kSrcRoot = 16u;       // the src trie root follows the 16-word blob header
 constexpr uint32_t kWalkKeyLimit = 0x30000u;  // keys >= this (ANY protocol) take the linear path
 // key bound of records that match every key: covers the whole 18-bit walk range, ANY keys

@@ -27,6 +27,9 @@ namespace pg {
 #ifndef PG_AGG_ROUNDS  // wave-aggregation rounds of hit-counter increments (Hist::inc)
 #define PG_AGG_ROUNDS 0
 #endif
+#ifndef PG_NODE_BF  // node evaluations: table-info reads without per-tuple branches
+#define PG_NODE_BF 1
+#endif
 #ifndef PG_NODE_FB_Q1  // node kernels: per-table fallback one tuple at a time
 #define PG_NODE_FB_Q1 1
 #endif
@@ -69,6 +72,9 @@ PG_NOINLINE uint32_t eval_linear(const DevRule* rules, uint32_t base, uint32_t n
 struct DevLoader {
     const uint32_t* b;
     PG_HD uint32_t u32(uint32_t i) const { return b[i]; }
+    PG_HD uint32_t at_byte(uint32_t off) const {
+        return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(b) + off);
+    }
     PG_HD W2 u2(uint32_t i) const {
 #if defined(__HIP_DEVICE_COMPILE__)
         const uint2 v = *reinterpret_cast<const uint2*>(b + i);
@@ -224,14 +230,12 @@ struct TabEval {
 // cover, LINEAR tables and ANY-protocol packets take the per-table path.
 // Q trie lookups in lockstep (root stride s1 over a W-bit address, then each node's stride).
 // PRED: one load per tuple per level, no per-tuple branches (LDS images).
+// Node-image encoding of the non-leaf entries (blobwalk.hpp node_entry).
 template <bool PRED, class L, int Q>
 PG_HD void node_trie_q(const L& ld, uint32_t root, uint32_t s1, uint32_t W, const uint32_t (&a)[Q], uint32_t (&c)[Q]) {
-    uint32_t sh[Q], e[Q];
+    uint32_t e[Q];
     PG_UNROLL
-    for (int j = 0; j < Q; j++) {
-        sh[j] = W - s1;
-        e[j] = ld.u32(root + (a[j] >> sh[j]));
-    }
+    for (int j = 0; j < Q; j++) e[j] = ld.u32(root + (a[j] >> (W - s1)));
     for (;;) {
         bool more = false;
         PG_UNROLL
@@ -241,16 +245,12 @@ PG_HD void node_trie_q(const L& ld, uint32_t root, uint32_t s1, uint32_t W, cons
         for (int j = 0; j < Q; j++) {
             if (PRED) {
                 const bool d = !(e[j] & kLeaf);
-                const uint32_t st = d ? trie_stride(e[j]) : 0u, ns = sh[j] - st;
-                const uint32_t v = ld.u32(d ? trie_child(e[j]) + ((a[j] >> ns) & ((1u << st) - 1u)) : 0u);
+                const uint32_t v = ld.at_byte(d ? node_child_byte(e[j], a[j]) : 0u);
                 e[j] = d ? v : e[j];
-                sh[j] = d ? ns : sh[j];
                 continue;
             }
             if (e[j] & kLeaf) continue;
-            const uint32_t st = trie_stride(e[j]);
-            sh[j] -= st;
-            e[j] = ld.u32(trie_child(e[j]) + ((a[j] >> sh[j]) & ((1u << st) - 1u)));
+            e[j] = ld.at_byte(node_child_byte(e[j], a[j]));
         }
     }
     PG_UNROLL
@@ -297,6 +297,25 @@ struct NodeEval {
         const uint32_t(&gk)[Q] = rev ? gack : gsyn;
         bool on[Q], fb[Q], pend[Q], cm[Q];
         uint32_t pos[Q];
+#if PG_NODE_BF
+        // branch-free: every lane reads its (or table 0's) image words, the flags select
+        PG_UNROLL
+        for (int j = 0; j < Q; j++) {
+            const uint32_t tt = act[j] ? (uint32_t)t[j] : 0u;
+            const W4 ti = img.u4(N.tabinfo + 4u * tt);  // {cross base, nkc | covered << 31, common row, 0}
+            const uint32_t ki = tt * N.gk + gk[j];
+            const uint32_t lk = (img.u32(N.kmap + (ki >> 1)) >> ((ki & 1u) * 16u)) & 0xFFFFu;
+            uint32_t cw = 0;
+            if (CM) {
+                const uint32_t b = tt * N.n_ipc + ca[j];
+                cw = img.u32(N.cmap + (b >> 5u)) >> (b & 31u);
+            }
+            on[j] = act[j] && k[j] < kWalkKeyLimit && (ti.y >> 31);
+            cm[j] = CM && (cw & 1u);
+            pos[j] = cm[j] ? ti.z + lk : ti.x + ca[j] * (ti.y & 0xFFFFu) + lk;
+            fb[j] = act[j] && !on[j];
+        }
+#else
         PG_UNROLL
         for (int j = 0; j < Q; j++) {
             on[j] = cm[j] = false;
@@ -319,6 +338,7 @@ struct NodeEval {
             }
             fb[j] = act[j] && !on[j];
         }
+#endif
         PG_UNROLL
         for (int j = 0; j < Q; j++) {
             pend[j] = false;

@@ -43,7 +43,8 @@ struct DevTable {          // 32 B: two 16-B loads
 // Node classifier (fastpath.cpp build_node; PERPOD / CONN modes): every table the node
 // covers evaluated through one IPv4 trie and one L4-key trie shared by all tables, and one
 // cross-table entry per evaluation.
-//   img    u32[]  IPv4 trie (root at word 0, leaf = node IP class) | L4-key trie (leaf = node
+//   img    u32[]  (tries: non-leaf entries in the node encoding, blobwalk.hpp node_entry)
+//                 IPv4 trie (root at word 0, leaf = node IP class) | L4-key trie (leaf = node
 //                 key class) | ipinfo uint2[n_ipc] {interface, tin | tout << 16} | tabinfo
 //                 uint4[T] {cross base, nkc | covered << 31, common row, 0} | kmap u16[T][gk]
 //                 (local key class) | the words up to img_words_base are the base image;

@@ -68,8 +68,11 @@ struct VecHash {
 constexpr uint32_t kTrieFail = 0xFFFFFFFFu;
 uint32_t g_lc_dense12 = 16;  // boundaries in a child's span that earn it a 12-bit stride
 constexpr uint32_t kLcRootBits = 14;  // HBM-resident blobs: the root alone is staged in LDS (64 KiB)
+// `node`: the node image's encoding (blobwalk.hpp node_child): a non-leaf entry holds the
+// child's BYTE offset << 10 | stride << 5 | the address shift of the child level, so a step is
+// one bit-field extract and one shifted add; children must lie below 2 MiB.
 uint32_t build_trie(std::vector<uint32_t>& blob, const std::vector<uint64_t>& bnd, const std::vector<uint32_t>& cls,
-                    uint32_t W, uint32_t s1, bool lc = false) {
+                    uint32_t W, uint32_t s1, bool lc = false, bool node = false) {
     // interval index containing address a
     auto find = [&](uint64_t a) { return (size_t)(std::upper_bound(bnd.begin(), bnd.end(), a) - bnd.begin()) - 1; };
     struct Job {
@@ -106,9 +109,9 @@ uint32_t build_trie(std::vector<uint32_t>& blob, const std::vector<uint64_t>& bn
                 else if (inside >= g_lc_dense12) st = 12;
             }
             uint32_t child = (uint32_t)blob.size();
-            if ((uint64_t)child + (1ull << st) > kTrieChildMask) return kTrieFail;
+            if ((uint64_t)child + (1ull << st) > (node ? kNodeChildMaxWords : kTrieChildMask)) return kTrieFail;
             blob.resize(blob.size() + (1u << st), 0);
-            blob[j.block + e] = child | (st << kTrieStrideShift);
+            blob[j.block + e] = node ? node_entry(child, st, j.shift - st) : child | (st << kTrieStrideShift);
             stack.push_back({child, a, j.shift - st, st});
         }
     }
@@ -672,9 +675,9 @@ bool build_node(HostTableSet& h, const std::vector<TableAnalysis*>& an, const st
     std::vector<uint32_t>& img = h.node_img;
     DevNode& N = h.node;
     N.ip_s1 = std::min(pick_stride(gb.size(), 32), g_node_root_bits);
-    if (build_trie(img, gb, gcls, 32, N.ip_s1, g_lc_node != 0) != 0) return false;
+    if (build_trie(img, gb, gcls, 32, N.ip_s1, g_lc_node != 0, true) != 0) return false;
     N.key_k1 = std::min(pick_stride(kb.size(), 18), g_node_root_bits);
-    N.key_root = build_trie(img, kb, kcls, 18, N.key_k1);
+    N.key_root = build_trie(img, kb, kcls, 18, N.key_k1, false, true);
     if (N.key_root == kTrieFail) return false;
     while (img.size() % 2) img.push_back(0);
     N.ipinfo = (uint32_t)img.size();
