@@ -154,7 +154,10 @@ def pmc_traffic(config, n, counters):
     (profiles/rNN_*_config<C>_pmc.json, FETCH_SIZE/WRITE_SIZE passes, gfx950-corrected by
     tools/prof_summary.py), scaled to this launch's tuple count; None when there is none."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_config%d_pmc.json" % config)))
+    import re
+    # newest round / version first by number (r01_v12 after r01_v9)
+    nat = lambda p: [int(x) if x.isdigit() else x for x in re.split(r"(\d+)", os.path.basename(p))]
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_config%d_pmc.json" % config)), key=nat)
     if not files or counters:
         return None, None
     with open(files[-1]) as f:
