@@ -289,13 +289,21 @@ struct NodeEval {
     const H& hook;
     bool* hooked;
     PG_HD void operator()(const int32_t (&t)[Q], const bool (&act)[Q], bool rev, uint32_t (&w)[Q]) const {
+        bool on[Q], fb[Q];
+        first(t, act, rev, on, fb, w);
+        rest(t, rev, on, fb, w);
+    }
+    // The first word of each evaluation (cross entry or common-row word) for the lanes the node
+    // covers (on), and which lanes need the per-table path (fb). It depends only on (t, rev):
+    // issuing testConnection's four evaluations this way up front was tried (A/B on MI355X,
+    // config 5: no gain at two tuples per chunk with counters, -4 % at one without).
+    PG_HD void first(const int32_t (&t)[Q], const bool (&act)[Q], bool rev, bool (&on)[Q], bool (&fb)[Q],
+                     uint32_t (&w)[Q]) const {
         const DevLoader X{N.cross};
-        const uint32_t(&a)[Q] = rev ? dst : src;
-        const uint32_t(&b)[Q] = rev ? src : dst;
         const uint32_t(&k)[Q] = rev ? kack : ksyn;
         const uint32_t(&ca)[Q] = rev ? cd : cs;
         const uint32_t(&gk)[Q] = rev ? gack : gsyn;
-        bool on[Q], fb[Q], pend[Q], cm[Q];
+        bool cm[Q];
         uint32_t pos[Q];
 #if PG_NODE_BF
         // branch-free: every lane reads its (or table 0's) image words, the flags select
@@ -341,7 +349,6 @@ struct NodeEval {
 #endif
         PG_UNROLL
         for (int j = 0; j < Q; j++) {
-            pend[j] = false;
             if (!on[j]) continue;
 #if defined(PG_PROBE_NOGATHER)  // measurement build only: no cross-entry load
             w[j] = pos[j] & 0x3FFFu;
@@ -364,8 +371,20 @@ struct NodeEval {
             __builtin_amdgcn_sched_barrier(0);
 #endif
         }
+    }
+    // the rest of the evaluations first() started: dst records of kNodeList words, the
+    // per-table path for fb lanes
+    PG_HD void rest(const int32_t (&t)[Q], bool rev, const bool (&on)[Q], const bool (&fb)[Q], uint32_t (&w)[Q]) const {
+        const DevLoader X{N.cross};
+        const uint32_t(&a)[Q] = rev ? dst : src;
+        const uint32_t(&b)[Q] = rev ? src : dst;
+        const uint32_t(&k)[Q] = rev ? kack : ksyn;
+        bool pend[Q];
+        uint32_t pos[Q];
         PG_UNROLL
         for (int j = 0; j < Q; j++) {
+            pend[j] = false;
+            pos[j] = 0;
             if (!on[j]) continue;
             pend[j] = (w[j] & kNodeList) != 0u;
             pos[j] = (w[j] & kNodeRecMask) << 2;

@@ -201,6 +201,9 @@ __device__ __forceinline__ void stream_store(V v, V* p) {
 #ifndef PG_QCONN
 #define PG_QCONN 1
 #endif
+#ifndef PG_QCONN_COUNT  // CONN with hit counters (A/B on MI355X, config 5: 2 = +9 % over 1, 4 = -6 %)
+#define PG_QCONN_COUNT 2
+#endif
 #ifndef PG_TPL  // tuples per lane per loop iteration (4 or 8)
 #define PG_TPL 4
 #endif
@@ -321,7 +324,7 @@ __global__ __launch_bounds__(BS) void k_classify(DevTableSet T, int32_t t, const
 #else
         // per-mode chunk: the group's P tuples are classified QC at a time (less state per
         // lane, more waves per SIMD)
-        constexpr int QC = MODE == 2 ? PG_QCONN : (MODE == 1 ? PG_QPOD : PG_QSINGLE);
+        constexpr int QC = MODE == 2 ? (COUNT ? PG_QCONN_COUNT : PG_QCONN) : (MODE == 1 ? PG_QPOD : PG_QSINGLE);
 #pragma unroll
         for (int c = 0; c < P; c += QC) {
             uint32_t cs[QC], cd[QC], csp[QC], cdp[QC], cpr[QC], co[QC];
