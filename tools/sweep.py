@@ -79,9 +79,10 @@ def main():
     name = os.path.basename(os.environ.get("VPP_AMD_LIB", "libpolicygpu.so"))
     for i, combo in enumerate(combos):
         ms = float(np.median(times[i]))
+        extra = {"blob": e.table_stats(w.table_id)} if w.mode == 0 and i == 0 else {}
         print(json.dumps({"lib": name, "config": a.config, "counters": a.counters, "pre": a.pre, "ns": a.ns, **dict(zip(keys, combo)), "ms": round(ms, 4),
                           "gpps": round(n / ms / 1e6, 1), "GBps": round(n * bpt / ms / 1e6, 1),
-                          "same_output": bool(torch.equal(outs[i], ref))}), flush=True)
+                          "same_output": bool(torch.equal(outs[i], ref)), **extra}), flush=True)
 
 
 if __name__ == "__main__":

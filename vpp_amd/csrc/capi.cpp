@@ -148,6 +148,11 @@ int pg_set_tuning(const char* key, int value) {
         set_lc_dense12((uint32_t)value);
         return PG_OK;
     }
+    if (std::string(key) == "lc_max_stride") {  // tables compiled afterwards
+        if (value != 12 && value != 16 && value != 18) return PG_EINVAL;
+        set_lc_max_stride((uint32_t)value);
+        return PG_OK;
+    }
     if (std::string(key) == "pair") {  // tables compiled afterwards
         if (value < 0 || value > 2) return PG_EINVAL;
         set_pair_enable((uint32_t)value);

@@ -127,6 +127,7 @@ void set_node_common(uint32_t on);  // common-row section of the node image (ima
 void set_pair_enable(uint32_t on);  // PAIR mode for tables CROSS cannot take (tables compiled afterwards)
 void set_lc_node(uint32_t on);  // level-compressed node IPv4 trie (tables compiled afterwards)
 void set_lc_lds(uint32_t on);
+void set_lc_max_stride(uint32_t s);  // widest level-compressed stride (12, 16 or 18; default 16)
 void set_lc_dense12(uint32_t n);  // level-compression threshold for 12-bit strides (default 256)   // level-compressed tries also for LDS-staged blobs that stay <= 64 KiB
 
 struct GenParams {         // device view of pg_gen_spec

@@ -64,9 +64,12 @@ struct VecHash {
 // and stride (blobwalk.hpp trie_child/trie_stride); children take 8-bit strides, or with
 // `lc` (level compression, for tries read from HBM) 18 / 16 / 12 bits when their span holds
 // at least 8192 / 2048 / 256 interval boundaries: about the memory of the 8-bit levels they
-// replace, one or two dependent loads fewer.
+// replace, one or two dependent loads fewer. 18-bit strides only when g_lc_max_stride allows
+// (off by default: a 1 MiB child per 2^18 span made config 4's blob 13.8 MB, over the 4 MB
+// L2 of an XCD; at 16 it is 6.2 MB and 4 % faster).
 constexpr uint32_t kTrieFail = 0xFFFFFFFFu;
 uint32_t g_lc_dense12 = 16;  // boundaries in a child's span that earn it a 12-bit stride
+uint32_t g_lc_max_stride = 16;  // widest stride level compression may pick (A/B on MI355X, config 4: 16 = +4 % over 18, 12 = -3 %)
 constexpr uint32_t kLcRootBits = 14;  // HBM-resident blobs: the root alone is staged in LDS (64 KiB)
 // `node`: the node image's encoding (blobwalk.hpp node_child): a non-leaf entry holds the
 // child's BYTE offset << 10 | stride << 5 | the address shift of the child level, so a step is
@@ -104,8 +107,8 @@ uint32_t build_trie(std::vector<uint32_t>& blob, const std::vector<uint64_t>& bn
             uint32_t st = std::min<uint32_t>(8, j.shift);
             if (lc && j.shift >= 12) {
                 const size_t inside = (size_t)(std::lower_bound(bnd.begin(), bnd.end(), a + span) - bnd.begin()) - k - 1;
-                if (j.shift >= 18 && inside >= 8192) st = 18;
-                else if (j.shift >= 16 && inside >= 2048) st = 16;
+                if (g_lc_max_stride >= 18 && j.shift >= 18 && inside >= 8192) st = 18;
+                else if (g_lc_max_stride >= 16 && j.shift >= 16 && inside >= 2048) st = 16;
                 else if (inside >= g_lc_dense12) st = 12;
             }
             uint32_t child = (uint32_t)blob.size();
@@ -163,6 +166,7 @@ void set_root_bits_max(uint32_t bits) { g_root_bits_max = std::max<uint32_t>(4, 
 void set_lc_node(uint32_t on) { g_lc_node = on; }
 void set_pair_enable(uint32_t on) { g_pair_enable = on; }
 void set_lc_dense12(uint32_t n) { g_lc_dense12 = n; }
+void set_lc_max_stride(uint32_t s) { g_lc_max_stride = s; }
 void set_node_common(uint32_t on) { g_node_common = on; }
 void set_node_tuning(uint32_t enable, uint32_t root_bits) {
     g_node_enable = enable;
