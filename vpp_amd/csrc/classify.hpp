@@ -257,6 +257,46 @@ PG_HD void node_trie_q(const L& ld, uint32_t root, uint32_t s1, uint32_t W, cons
     for (int j = 0; j < Q; j++) c[j] = e[j] & ~kLeaf;
 }
 
+// Two tries of the node image walked in one lockstep loop (IPv4 addresses a over the root at
+// 0, L4 keys b over the key root): the walks are independent, so their dependent LDS reads
+// overlap instead of running one trie after the other. Below the roots a step needs only the
+// entry and the address (node_child_byte), whichever trie it belongs to.
+template <bool PRED, class L, int QA, int QB>
+PG_HD void node_trie2_q(const L& ld, const DevNode& N, const uint32_t (&a)[QA], uint32_t (&ca)[QA],
+                        const uint32_t (&b)[QB], uint32_t (&cb)[QB]) {
+    constexpr int Q = QA + QB;
+    uint32_t x[Q], e[Q];
+    PG_UNROLL
+    for (int j = 0; j < QA; j++) x[j] = a[j], e[j] = ld.u32(a[j] >> (32u - N.ip_s1));
+    PG_UNROLL
+    for (int j = 0; j < QB; j++) x[QA + j] = b[j], e[QA + j] = ld.u32(N.key_root + (b[j] >> (18u - N.key_k1)));
+    for (;;) {
+        bool more = false;
+        PG_UNROLL
+        for (int j = 0; j < Q; j++) more |= !(e[j] & kLeaf);
+        if (!more) break;
+        PG_UNROLL
+        for (int j = 0; j < Q; j++) {
+            if (PRED) {
+                const bool d = !(e[j] & kLeaf);
+                const uint32_t v = ld.at_byte(d ? node_child_byte(e[j], x[j]) : 0u);
+                e[j] = d ? v : e[j];
+                continue;
+            }
+            if (e[j] & kLeaf) continue;
+            e[j] = ld.at_byte(node_child_byte(e[j], x[j]));
+        }
+    }
+    PG_UNROLL
+    for (int j = 0; j < QA; j++) ca[j] = e[j] & ~kLeaf;
+    PG_UNROLL
+    for (int j = 0; j < QB; j++) cb[j] = e[QA + j] & ~kLeaf;
+}
+
+#ifndef PG_NODE_WALK2  // node kernels: IPv4 and key tries in one lockstep walk
+#define PG_NODE_WALK2 1
+#endif
+
 // end point of a node IP class (ipinfo: {interface, tin | tout << 16}, 0xFFFF = no ACL)
 template <class L>
 PG_HD End node_end(const L& img, const DevNode& N, uint32_t ipc) {
@@ -596,13 +636,33 @@ PG_HD void classify_node_q(const DevTableSet& T, const DevNode& N, const L& img,
     uint32_t ips[2 * Q], ipc[2 * Q];
     PG_UNROLL
     for (int j = 0; j < Q; j++) ips[j] = s[j], ips[Q + j] = d[j];
+    uint32_t cs[Q], cd[Q], gs[Q], ga[Q];
+#if PG_NODE_WALK2 && !defined(PG_PROBE_NOWALK)
+    if (MODE == 2) {
+        uint32_t keys[2 * Q], kc[2 * Q];
+        PG_UNROLL
+        for (int j = 0; j < Q; j++) {
+            keys[j] = key[j] < kWalkKeyLimit ? key[j] : 0u;
+            keys[Q + j] = kack[j] < kWalkKeyLimit ? kack[j] : 0u;
+        }
+        node_trie2_q<PRED>(img, N, ips, ipc, keys, kc);
+        PG_UNROLL
+        for (int j = 0; j < Q; j++) gs[j] = kc[j], ga[j] = kc[Q + j];
+    } else {
+        uint32_t keys[Q];
+        PG_UNROLL
+        for (int j = 0; j < Q; j++) keys[j] = key[j] < kWalkKeyLimit ? key[j] : 0u;
+        node_trie2_q<PRED>(img, N, ips, ipc, keys, gs);
+        PG_UNROLL
+        for (int j = 0; j < Q; j++) ga[j] = gs[j];
+    }
+#else
 #if defined(PG_PROBE_NOWALK)  // measurement build only: IP classes without the trie walk
     PG_UNROLL
     for (int j = 0; j < 2 * Q; j++) ipc[j] = ips[j] % N.n_ipc;
 #else
     node_trie_q<PRED>(img, 0u, N.ip_s1, 32u, ips, ipc);
 #endif
-    uint32_t cs[Q], cd[Q], gs[Q], ga[Q];
     if (MODE == 2) {
         uint32_t keys[2 * Q], kc[2 * Q];
         PG_UNROLL
@@ -621,6 +681,7 @@ PG_HD void classify_node_q(const DevTableSet& T, const DevNode& N, const L& img,
         PG_UNROLL
         for (int j = 0; j < Q; j++) ga[j] = gs[j];
     }
+#endif
     PG_UNROLL
     for (int j = 0; j < Q; j++) cs[j] = ipc[j], cd[j] = ipc[Q + j];
     bool hooked = false;
