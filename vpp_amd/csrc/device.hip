@@ -236,8 +236,12 @@ __device__ __forceinline__ void st_words(const Words<NW>& v, uint32_t* p) {
     for (int k = 0; k < NW / 4; k++)
         stream_store(v4u{v.w[4 * k], v.w[4 * k + 1], v.w[4 * k + 2], v.w[4 * k + 3]}, reinterpret_cast<v4u*>(p) + k);
 }
+#ifndef PG_NODE_WPE  // node kernels: minimum waves per SIMD the register allocation must allow (1 = any)
+#define PG_NODE_WPE 1
+#endif
 template <int MODE, bool COUNT, bool VEC, int STAGE, bool NODE, int BS>
-__global__ __launch_bounds__(BS) void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
+__global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(NODE ? PG_NODE_WPE : 1)))
+void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
                                                      const uint32_t* __restrict__ dst,
                                                      const uint16_t* __restrict__ sport,
                                                      const uint16_t* __restrict__ dport,
