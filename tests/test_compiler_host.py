@@ -136,3 +136,30 @@ def test_empty_and_catch_all_tables():
     tup = fz.rand_tuples(np.random.default_rng(1), 5000, fz.ANCHORS, any_pct=0.1)
     check(e, "empty", [], tup)
     check(e, "all", [{"action": 2, "src": "", "dst": ""}], tup)
+
+
+def test_candidate_mode_multi_record_lists():
+    """CAND lists of several candidates (nested src prefixes, dst-specific rules) whose last
+    record carries the last-record flag instead of a match-all terminator, empty lists
+    (sources no rule covers), and unconditional rules that end a list early."""
+    rnd = random.Random(23)
+    rules = []
+    for k in range(17000):
+        a, b = rnd.randrange(8), rnd.randrange(64)
+        src = rnd.choice(["10.%d.0.0/16" % a, "10.%d.%d.0/24" % (a, b), "10.%d.%d.%d/30" % (a, b, 4 * rnd.randrange(64))])
+        r = {"action": rnd.randrange(2), "src": src,
+             "dst": rnd.choice(["", "", "192.168.%d.0/24" % rnd.randrange(4), "192.168.0.%d/32" % rnd.randrange(8)])}
+        kind = rnd.random()
+        if kind < 0.45:
+            lo = rnd.randrange(1, 60000)
+            r["tcp"] = {"src": [0, 65535], "dst": [lo, lo + rnd.choice([0, 3, 100])]}
+        elif kind < 0.9:
+            lo = rnd.randrange(1, 60000)
+            r["udp"] = {"src": [0, 65535], "dst": [lo, lo + rnd.choice([0, 3, 100])]}
+        rules.append(r)
+    e = engine_with({"big": rules})
+    assert e.table_stats(0)["structure"] == "cand"
+    anchors = [(10 << 24) | (a << 16) | (b << 8) for a in range(9) for b in range(0, 66, 3)] + \
+              [(192 << 24) | (168 << 16) | (k << 8) for k in range(5)]
+    tup = fz.rand_tuples(np.random.default_rng(24), 30000, anchors)
+    check(e, "big", rules, tup)

@@ -66,9 +66,12 @@ struct BlobTab {
     uint32_t nkc;    // key classes
 };
 
-// Record (16 B): {dnet, klo | dlen << 18, khi, verdict}: matches when the dst prefix of
-// length dlen equals dnet and klo <= key <= khi. Candidate lists (CAND) and dst lists (LISTS)
-// end with a record that matches every packet and carries the fall-through verdict.
+// Record (16 B): {dnet, klo | dlen << 18 | last << 24, khi, verdict}: matches when the dst
+// prefix of length dlen equals dnet and klo <= key <= khi. Dst lists (LISTS, node lists) end
+// with a record that matches every packet and carries the fall-through verdict; candidate
+// lists (CAND) instead flag their last record (kRecLast): no match there -> the table's
+// default deny (an empty candidate list is one match-all record carrying it).
+constexpr uint32_t kRecLast = 1u << 24;
 PG_HD uint32_t rec_mask(uint32_t dlen) { return dlen ? (0xFFFFFFFFu << (32u - dlen)) : 0u; }
 PG_HD bool rec_match(const W4& r, uint32_t dst, uint32_t key) {
     return (dst & rec_mask((r.y >> 18) & 63u)) == r.x && key >= (r.y & 0x3FFFFu) && key <= r.z;
@@ -186,6 +189,9 @@ PG_HD void blob_walk(const L (&ld)[Q], const L0 (&ld0)[Q], const BlobTab (&tb)[Q
             const W4 r = ld[j].u4(pos[j]);
             if (rec_match(r, dst[j], key[j])) {
                 w[j] = r.w;
+                pend[j] = false;
+            } else if (r.y & kRecLast) {
+                w[j] = tb[j].dflt;
                 pend[j] = false;
             } else {
                 pos[j] += 4u;

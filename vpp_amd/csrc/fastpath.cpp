@@ -514,7 +514,7 @@ bool build_fast_table(const DevRule* rules, uint32_t n, uint32_t rule_base, uint
     uint64_t nrec = 0;
     for (uint32_t s = 0; s < nsc; s++) {
         first_rec[s] = (uint32_t)nrec;
-        nrec += src_lists[s].size() + 1;
+        nrec += std::max<size_t>(src_lists[s].size(), 1);
     }
     if (nrec >= (1ull << 29)) return false;
     std::vector<uint32_t> leaf(sb.size());
@@ -527,12 +527,15 @@ bool build_fast_table(const DevRule* rules, uint32_t n, uint32_t rule_base, uint
     while (blob.size() % 4) blob.push_back(0);  // 16-byte records
     blob[6] = (uint32_t)blob.size();
     for (uint32_t s = 0; s < nsc; s++) {
-        for (uint32_t r : src_lists[s]) {
+        const std::vector<uint32_t>& L = src_lists[s];
+        for (size_t i = 0; i < L.size(); i++) {
+            const uint32_t r = L[i];
             uint32_t l = 0;
             dlen(rules[r].dmask, &l);
-            put_rec(rules[r].dnet, l, rules[r].klo, rules[r].khi, verdict(r));
+            // the last candidate carries kRecLast: no match -> the table's default deny
+            put_rec(rules[r].dnet, l | (i + 1 == L.size() ? kRecLast >> 18 : 0u), rules[r].klo, rules[r].khi, verdict(r));
         }
-        put_rec(0, 0, 0, kRecKeyAll, dflt);  // no candidate matched: the table's default deny
+        if (L.empty()) put_rec(0, 0, 0, kRecKeyAll, dflt);  // no candidate: the table's default deny
     }
     return true;
 }
