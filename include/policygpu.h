@@ -147,10 +147,13 @@ pg_ctx* pg_create(int hip_device);
  * image staged in LDS, default 16384), "block_stage" (workgroup size of LDS-staged
  * classify launches: 256, 512 or 1024; default 0 = per mode),
  * "lc_lds" (table blobs of at least this many words are rebuilt with level-compressed
- * 12/16/18-bit trie strides and keep them when the result still fits in LDS; default 4096,
+ * 12/16-bit trie strides and keep them when the result still fits in LDS; default 4096,
  * 0 = off; blobs too large for LDS are always level-compressed), "lc_dense12" (boundaries a
- * subtree needs for a 12-bit stride, default 16), "lc_node" (1/0: level-compressed node
- * tries, default 0), "pair" (1/0: the PAIR structure -- src x dst classes, then x key
+ * subtree needs for a 12-bit stride, default 16), "lc_max_stride" (widest level-compressed
+ * stride: 12, 16 or 18, default 16), "lc_node" (1/0: level-compressed node
+ * tries, default 0), "node_common" (1/0: common-row section of node images, default 1),
+ * "node_common_lds_max" (LDS bytes up to which that section is staged, default 80 KiB),
+ * "pair" (1/0: the PAIR structure -- src x dst classes, then x key
  * classes -- for tables the cross product cannot take, default 1; 0 = candidate lists;
  * 2 = wherever it fits, for tests)
  * -- tables compiled afterwards */
