@@ -192,8 +192,14 @@ __device__ __forceinline__ void stream_store(V v, V* p) {
 #define PG_PRED 0
 #endif
 // tuples of a group classified together (lockstep chunk), per mode, each dividing PG_TPL
+// SINGLE: blob staged in LDS (STAGE 1) one tuple at a time, blob in HBM two (A/B on MI355X:
+// config 2 331 / 343 / 348 Gpps at 4 / 2 / 1, with counters 307 / 316 / 325; config 4 119 /
+// 121.5 / 113.5)
+#ifndef PG_QSINGLE_LDS
+#define PG_QSINGLE_LDS 1
+#endif
 #ifndef PG_QSINGLE
-#define PG_QSINGLE 4
+#define PG_QSINGLE 2
 #endif
 #ifndef PG_QPOD
 #define PG_QPOD 4
@@ -328,7 +334,8 @@ void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
 #else
         // per-mode chunk: the group's P tuples are classified QC at a time (less state per
         // lane, more waves per SIMD)
-        constexpr int QC = MODE == 2 ? (COUNT ? PG_QCONN_COUNT : PG_QCONN) : (MODE == 1 ? PG_QPOD : PG_QSINGLE);
+        constexpr int QC = MODE == 2 ? (COUNT ? PG_QCONN_COUNT : PG_QCONN)
+                                     : (MODE == 1 ? PG_QPOD : (STAGE == 1 ? PG_QSINGLE_LDS : PG_QSINGLE));
 #pragma unroll
         for (int c = 0; c < P; c += QC) {
             uint32_t cs[QC], cd[QC], csp[QC], cdp[QC], cpr[QC], co[QC];
