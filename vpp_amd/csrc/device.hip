@@ -575,9 +575,10 @@ static void launch_one(const DevTableSet& T, int t, const uint32_t* src, const u
                        const uint16_t* dport, const uint8_t* proto, uint64_t n, uint32_t* out,
                        unsigned long long* counters, hipStream_t st, size_t hist, uint32_t stage, uint64_t items) {
     if constexpr (STAGE) {
-        // 512 for every mode (A/B on MI355X: SINGLE with counters +14 % over 1024 at config 2;
-        // without counters +2.5 % since SINGLE classifies one tuple per chunk, v15)
-        const uint32_t bs = g_block_stage ? g_block_stage : 512u;
+        // 512 (A/B on MI355X: SINGLE with counters +14 % over 1024 at config 2; without
+        // counters +2.5 % since SINGLE classifies one tuple per chunk, v15), except SINGLE
+        // without counters over an HBM blob with its root staged: 1024 (config 4 +1.3 %)
+        const uint32_t bs = g_block_stage ? g_block_stage : (MODE == 0 && !COUNT && STAGE == 2 ? 1024u : 512u);
         if (bs == 1024u)
             return launch_bs<MODE, COUNT, VEC, STAGE, NODE, 1024>(T, t, src, dst, sport, dport, proto, n, out, counters,
                                                                   st, hist, stage, items);
