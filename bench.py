@@ -36,11 +36,16 @@ MODE_NAME = {0: "single", 1: "perpod", 2: "conn"}
 
 def parse():
     p = argparse.ArgumentParser()
-    p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=200)
-    p.add_argument("--warmup", type=int, default=50)
+    p.add_argument("--gpus", type=int, default=1,
+                   help="GPUs = ranks; > 1 without a torchrun environment re-launches under torchrun")
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--config", type=int, default=2, choices=sorted(W.CONFIGS))
-    p.add_argument("--tuples", type=int, default=0, help="tuples per GPU (default: the config's)")
+    p.add_argument("--tuples", type=int, default=0, help="tuples per GPU (weak scaling; default: the config's)")
+    p.add_argument("--scaling", choices=("weak", "strong"), default="weak",
+                   help="weak: --tuples per GPU; strong: --total-tuples split over the GPUs")
+    p.add_argument("--total-tuples", type=int, default=0,
+                   help="strong scaling: tuples of the whole job (default 8 x the config's per-GPU count)")
     p.add_argument("--counters", action="store_true", help="time with per-rule hit counters on")
     p.add_argument("--cpu-sample", type=int, default=16 << 20, help="tuples in the CPU-baseline sample")
     p.add_argument("--faithful-seconds", type=float, default=8.0,
@@ -48,25 +53,57 @@ def parse():
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--per-table", action="store_true",
                    help="PERPOD/CONN through the per-table blobs + IP hash instead of the node classifier")
+    p.add_argument("--cpu-dry-run", action="store_true",
+                   help="no GPU: the launcher, sharding, timing and counter all-reduce over gloo, with the "
+                        "product's per-tuple code run on the host (tests only; no throughput claim)")
     return p.parse_args()
+
+
+def relaunch(a):
+    """--gpus N > 1 started as a plain process: run this script under torchrun (one rank per GPU)
+    as a child -- before anything touches the GPU -- and exit with its status."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=%d" % a.gpus,
+           "--master-addr=127.0.0.1", "--master-port=%d" % port, os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    return subprocess.call(cmd, env=env)
+
+
+def shard_of(a, w, rank, world):
+    """global tuple-index range of this rank"""
+    if a.scaling == "strong":
+        total = a.total_tuples or 8 * w.n_tuples
+        return VD.shard_strong(rank, world, total)
+    return VD.shard(rank, world, a.tuples or w.n_tuples)
 
 
 def main():
     a = parse()
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(relaunch(a))
     rank, world, local = VD.env()
+    if world != a.gpus:
+        raise SystemExit("bench.py: --gpus %d but the launcher started %d ranks" % (a.gpus, world))
+    if a.cpu_dry_run:
+        return dry_run(a, rank, world)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     else:
         torch.cuda.set_device(local)
-    if a.per_table:
-        assert _capi.lib.pg_set_tuning(b"node_path", 0) == 0
     kw = {"n_tuples": a.tuples} if a.tuples else {}
     w = W.CONFIGS[a.config](local, **kw)
-    e, n = w.engine, w.n_tuples
+    e = w.engine
+    if a.per_table:
+        e.set_tuning("node_path", 0)
     st = w.stats()
-    base, n = VD.shard(rank, world, n)  # weak scaling: n tuples per rank, disjoint global ranges
+    base, n = shard_of(a, w, rank, world)  # disjoint global index ranges
     b = D.TupleBatch(n, with_sport=(w.mode == 2))
     D.gen_tuples(e, b, index_base=base, **w.gen)
     out = torch.empty(n, dtype=torch.int32, device="cuda")
@@ -100,38 +137,109 @@ def main():
     kern_ms = ev0.elapsed_time(ev1) / a.steps
     wall = VD.max_over_ranks(wall, "cuda")
     ms_per_step = wall * 1e3 / a.steps
-    total_tuples = n * world * a.steps
+    total_tuples = VD.sum_over_ranks(n, "cuda") * a.steps
     mpps = total_tuples / wall / 1e6
 
-    # statscollector path: one RCCL all-reduce of the per-rule hit counters
-    allreduce_ms = None
+    # statscollector path: the per-rule hit counters of one counted pass over every rank's
+    # shard, summed by RCCL through the library's own communicator (pg_allreduce_counters)
+    allreduce = None
     if world > 1:
-        D.classify(e, w.mode, w.table_id, b, out, counters=counters)
-        torch.cuda.synchronize()
-        dist.barrier()
-        t1 = time.perf_counter()
-        VD.allreduce_counters(counters)
-        torch.cuda.synchronize()
-        allreduce_ms = (time.perf_counter() - t1) * 1e3
+        allreduce = counter_allreduce(e, w, b, out, rank, world)
 
     achieved = n * BYTES_PER_TUPLE[w.mode] / (kern_ms * 1e-3) / 1e9
     traffic, traffic_src = pmc_traffic(a.config, n, a.counters and not w.counters)
     line = {
         "metric": METRIC, "value": round(mpps, 1), "unit": "Mpps", "n_gpus": world, "steps": a.steps,
-        "warmup": a.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True, "scaling": "weak",
+        "warmup": a.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True, "scaling": a.scaling,
         "vs_baseline": None, "dtype": "u32", "data": "synthetic (device-generated, counter-based splitmix64)",
         "config": {"workload": "config%d: %s" % (a.config, w.desc), "mode": MODE_NAME[w.mode],
-                   "tuples_per_gpu": n, "rules": st["rules"], "tables": st["tables"], "parallelism": "dp%d" % world,
+                   "tuples_per_gpu": n, "tuples_total": total_tuples // a.steps, "rules": st["rules"],
+                   "tables": st["tables"], "parallelism": "dp%d" % world,
                    "counters": bool(use_counters), "classifier": classifier(w, a.per_table)},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "bytes_per_tuple": BYTES_PER_TUPLE[w.mode], "kernel_ms": round(kern_ms, 4),
                      "algorithmic_bytes_per_launch": n * BYTES_PER_TUPLE[w.mode], "traffic_source": traffic_src},
     }
-    if allreduce_ms is not None:
-        line["counter_allreduce_ms"] = round(allreduce_ms, 3)
+    if allreduce is not None:
+        line.update(allreduce)
     if rank == 0 and world == 1 and not a.no_cpu:
         line["cpu_baseline"], line["parity_sample"] = cpu_baseline(w, b, out, a.cpu_sample, a.faithful_seconds)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def counter_allreduce(e, w, b, out, rank, world):
+    """One counted classify pass per rank into the context's own counters, then
+    pg_allreduce_counters over an RCCL communicator the library holds (unique id from rank 0
+    over torch.distributed). Returns the timing and a consistency check: every tuple of every
+    rank is counted (SINGLE / PERPOD: one evaluation per tuple; CONN: at least one)."""
+    res = {}
+    try:
+        uid = [D.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        D.comm_init_rank(e, world, uid[0], rank)
+        D.reset_counters(e)
+        D.classify(e, w.mode, w.table_id, b, out, counters=D.counters_device_ptr(e))
+        torch.cuda.synchronize()
+        dist.barrier()
+        t1 = time.perf_counter()
+        summed = D.allreduce_counters(e)
+        res["counter_allreduce_ms"] = round((time.perf_counter() - t1) * 1e3, 3)
+        total = VD.sum_over_ranks(b.n, "cuda")
+        got = int(summed.sum())
+        res["counter_allreduce_check"] = bool(got == total if w.mode != 2 else got >= total)
+        res["counter_slots"] = int(len(summed))
+    except Exception as ex:  # reported, not fatal: the throughput line still prints
+        res["counter_allreduce_error"] = str(ex)[:300]
+    return res
+
+
+def dry_run(a, rank, world):
+    """CPU rehearsal of the multi-rank path (gloo): same launcher, sharding, barriers,
+    max-over-ranks timing and counter all-reduce as on GPUs; the per-tuple code is the
+    product's, run on the host (pg_debug_classify_host); inputs are a numpy restatement of a
+    small random shard. Prints the same JSON line with "dry_run": true."""
+    import numpy as np
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    if world > 1:
+        dist.init_process_group("gloo")
+    kw = {"n_tuples": a.tuples or 1 << 14}
+    w = W.CONFIGS[a.config](0, **kw)
+    e = w.engine
+    base, n = shard_of(a, w, rank, world)
+    rng = np.random.default_rng([w.gen["seed"], base])
+    src = rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32)
+    dst = rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32)
+    pool = w.gen.get("ip_pool")
+    if pool is not None and len(pool):
+        m = rng.random(n) < 0.8
+        dst[m] = np.asarray(pool, np.uint32)[rng.integers(0, len(pool), int(m.sum()))]
+    sport = rng.integers(0, 1 << 16, n).astype(np.uint16)
+    dport = rng.integers(0, 1 << 16, n).astype(np.uint16)
+    proto = rng.integers(0, 3, n).astype(np.uint8)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(a.warmup + a.steps):
+        _, cnt = e.debug_classify_host(w.mode, w.table_id, src, dst, sport, dport, proto, counters=True)
+    if world > 1:
+        dist.barrier()
+    wall = VD.max_over_ranks(time.perf_counter() - t0, "cpu")
+    counters = torch.from_numpy(cnt.astype(np.int64))
+    t1 = time.perf_counter()
+    VD.allreduce_counters(counters)
+    total = VD.sum_over_ranks(n, "cpu")
+    line = {"metric": METRIC, "value": round(total * a.steps / wall / 1e6, 3), "unit": "Mpps", "n_gpus": world,
+            "steps": a.steps, "warmup": a.warmup, "scaling": a.scaling, "dry_run": True,
+            "config": {"workload": "config%d: %s" % (a.config, w.desc), "tuples_per_gpu": n, "tuples_total": total,
+                       "parallelism": "dp%d" % world},
+            "counter_allreduce_ms": round((time.perf_counter() - t1) * 1e3, 3),
+            "counter_allreduce_check": bool(int(counters.sum()) == total if w.mode != 2 else
+                                            int(counters.sum()) >= total),
+            "counters_sha": __import__("hashlib").sha1(counters.numpy().tobytes()).hexdigest()[:16]}
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:

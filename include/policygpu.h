@@ -134,29 +134,38 @@ typedef struct pg_ctx pg_ctx;
 typedef struct pg_renderer pg_renderer;
 typedef struct pg_txn pg_txn;
 
+/* One context per GPU. Every call that touches the device makes hip_device current for its
+ * duration and restores the caller's current device afterwards, so contexts on different GPUs
+ * can be driven from one process, and a cgo caller may call from any OS thread. A context is
+ * not re-entrant; distinct contexts may be used concurrently from different threads. */
 pg_ctx* pg_create(int hip_device);
-/* tuning (process-wide): "blocks_per_cu" (cap on resident workgroups per CU of the classify
- * grid; default 0 = as many as registers/LDS allow),
- * "stage_max_words" (largest table blob staged in LDS, default 16384 = 64 KiB),
- * "root_bits_max" (cap of the src/key trie root stride, 4..16, default 16; affects tables
- * compiled afterwards),
- * "node_build" (1/0: build the node classifier for PERPOD / CONN, default 1; tables compiled
- * afterwards), "node_root_bits" (its IPv4 / key trie root stride cap, default 12),
- * "node_path" (1/0: classify PERPOD / CONN through the node classifier when it exists,
- * default 1; 0 = per-table blobs and the IP hash), "node_stage_max_words" (largest node
- * image staged in LDS, default 16384), "block_stage" (workgroup size of LDS-staged
- * classify launches: 256, 512 or 1024; default 0 = per mode),
- * "lc_lds" (table blobs of at least this many words are rebuilt with level-compressed
- * 12/16-bit trie strides and keep them when the result still fits in LDS; default 4096,
- * 0 = off; blobs too large for LDS are always level-compressed), "lc_dense12" (boundaries a
- * subtree needs for a 12-bit stride, default 16), "lc_max_stride" (widest level-compressed
- * stride: 12, 16 or 18, default 16), "lc_node" (1/0: level-compressed node
- * tries, default 0), "node_common" (1/0: common-row section of node images, default 1),
- * "node_common_lds_max" (LDS bytes up to which that section is staged, default 80 KiB),
- * "pair" (1/0: the PAIR structure -- src x dst classes, then x key
- * classes -- for tables the cross product cannot take, default 1; 0 = candidate lists;
- * 2 = wherever it fits, for tests)
- * -- tables compiled afterwards */
+int pg_ctx_device(const pg_ctx* ctx);
+/* Tuning knobs (key, value):
+ * launches -- "blocks_per_cu" (cap on resident workgroups per CU of the classify grid;
+ * default 0 = as many as registers/LDS allow), "stage_max_words" (largest table blob staged
+ * in LDS, default 16384 = 64 KiB), "stage_root_max_words" (larger blobs: header + src-trie
+ * root staged, default 16400), "node_path" (1/0: classify PERPOD / CONN through the node
+ * classifier when it exists, default 1; 0 = per-table blobs and the IP hash),
+ * "node_stage_max_words" (largest node image staged in LDS, default 16384),
+ * "node_common_lds_max" (LDS bytes up to which the node image's common-row section is staged,
+ * default 80 KiB), "block_stage" (workgroup size of LDS-staged classify launches: 256, 512 or
+ * 1024; default 0 = per mode);
+ * table compiler (the context recompiles and re-uploads on its next use; hit counters restart)
+ * -- "root_bits_max" (cap of the src/key trie root stride, 4..16, default 16), "node_build"
+ * (1/0: build the node classifier for PERPOD / CONN, default 1), "node_root_bits" (its IPv4 /
+ * key trie root stride cap, default 12), "lc_lds" (table blobs of at least this many words are
+ * rebuilt with level-compressed 12/16-bit trie strides and keep them when the result still
+ * fits in LDS; default 4096, 0 = off; blobs too large for LDS are always level-compressed),
+ * "lc_dense12" (boundaries a subtree needs for a 12-bit stride, default 16), "lc_max_stride"
+ * (widest level-compressed stride: 12, 16 or 18, default 16), "lc_node" (1/0:
+ * level-compressed node tries, default 0), "node_common" (1/0: common-row section of node
+ * images, default 1), "pair" (1/0: the PAIR structure -- src x dst classes, then x key classes
+ * -- for tables the cross product cannot take, default 1; 0 = candidate lists; 2 = wherever it
+ * fits, for tests).
+ * pg_ctx_set_tuning sets one context's knob; pg_set_tuning sets the process default that
+ * contexts created afterwards start from. PG_EINVAL for an unknown key or a value out of range. */
+int pg_ctx_set_tuning(pg_ctx* ctx, const char* key, int value);
+int pg_ctx_get_tuning(const pg_ctx* ctx, const char* key, int* value); /* ctx NULL: process default */
 int pg_set_tuning(const char* key, int value);
 void pg_destroy(pg_ctx* ctx);
 const char* pg_last_error(const pg_ctx* ctx);
@@ -241,7 +250,32 @@ int pg_classify_linear(pg_ctx* ctx, int table_id, const pg_tuple_soa* tuples, ui
 /* device-resident per-rule hit counters (u64, pg_num_counter_slots entries) */
 uint64_t* pg_counters_device(pg_ctx* ctx);
 int pg_reset_counters(pg_ctx* ctx, void* hip_stream);
+/* waits for this context's classify launches, copies min(n, slots) counters -> slots copied
+ * (also refreshes the host snapshot) */
 int pg_read_counters(pg_ctx* ctx, uint64_t* host_out, size_t n);
+/* the host snapshot of the counters taken by the last pg_read_counters / pg_allreduce_counters*
+ * (cluster-wide after an all-reduce); never touches the GPU, so a pull-style statscollector
+ * gauge (RegisterGaugeFunc, plugin_impl_statscollector.go:248-261) can read it at scrape time.
+ * Copies min(n, slots) -> number of slots in the snapshot (0 before the first read). */
+int pg_counters_snapshot(const pg_ctx* ctx, uint64_t* host_out, size_t n);
+
+/* ---- RCCL over xGMI: per-rule hit counters summed over the GPUs of a node -------------
+ * (the statscollector path). The classify path itself has no exchange.
+ * Multi-process (one process per GPU): rank 0 calls pg_comm_unique_id and hands the bytes to
+ * the other ranks (any side channel), every rank calls pg_comm_init_rank on its context.
+ * One process driving several GPUs: pg_comm_init_all over one context per GPU.
+ * pg_allreduce_counters / pg_allreduce_counters_all first check that every rank compiled the
+ * same counter layout (slots, ACL names, rules per ACL; PG_EFAULT if not, nothing reduced), then
+ * sum the device counters in place (ncclAllReduce u64 sum) and refresh the host snapshots.
+ * Synchronous. RCCL (librccl.so.1) is loaded on first use. */
+#define PG_COMM_ID_BYTES 128
+int pg_comm_unique_id(uint8_t id[PG_COMM_ID_BYTES]);
+int pg_comm_init_rank(pg_ctx* ctx, int nranks, const uint8_t id[PG_COMM_ID_BYTES], int rank);
+int pg_comm_init_all(pg_ctx* const* ctxs, int n);
+int pg_comm_destroy(pg_ctx* ctx);
+int pg_comm_rank(const pg_ctx* ctx, int* rank, int* nranks); /* PG_ENOENT: no communicator */
+int pg_allreduce_counters(pg_ctx* ctx, void* hip_stream);
+int pg_allreduce_counters_all(pg_ctx* const* ctxs, int n);
 
 /* ---- synthetic input generation on device (bench / parity workloads) ----------------- */
 typedef struct pg_gen_spec {

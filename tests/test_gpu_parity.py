@@ -317,20 +317,12 @@ def test_k8s_object_cluster_gpu_vs_oracle(mode):
 
 
 def _classify_with(e, mode, b, node_path, stage_words=16384, counters=False, common_lds=80 << 10):
-    lib = R.lib
-    assert lib.pg_set_tuning(b"node_path", node_path) == 0
-    assert lib.pg_set_tuning(b"node_stage_max_words", stage_words) == 0
-    assert lib.pg_set_tuning(b"node_common_lds_max", common_lds) == 0
-    try:
+    with e.tuning(node_path=node_path, node_stage_max_words=stage_words, node_common_lds_max=common_lds):
         out = torch.empty(b.n, dtype=torch.int32, device="cuda")
         cnt = torch.zeros(e.num_counter_slots(), dtype=torch.int64, device="cuda") if counters else None
         D.classify(e, mode, -1, b, out, counters=cnt)
         torch.cuda.synchronize()
         return out.cpu().numpy().view(np.uint32), (cnt.cpu().numpy() if counters else None)
-    finally:
-        lib.pg_set_tuning(b"node_path", 1)
-        lib.pg_set_tuning(b"node_stage_max_words", 16384)
-        lib.pg_set_tuning(b"node_common_lds_max", 80 << 10)
 
 
 @pytest.mark.parametrize("config", [3, 5])
@@ -378,11 +370,8 @@ def test_large_table_root_staged_and_hbm_walks_equal_oracle():
     ea, es = expected_single(e, tid, rules, tup)
     outs = []
     for root_words in (16400, 0):
-        assert R.lib.pg_set_tuning(b"stage_root_max_words", root_words) == 0
-        try:
+        with e.tuning(stage_root_max_words=root_words):
             got, _ = run_single(e, tid, tup)
-        finally:
-            R.lib.pg_set_tuning(b"stage_root_max_words", 16400)
         assert ((got >> 30) == ea).all() and ((got & 0x3FFFFFFF) == es).all()
         outs.append(got)
     assert np.array_equal(outs[0], outs[1])

@@ -64,7 +64,7 @@ def main():
     for r in range(a.rounds):
         for i, combo in enumerate(combos):
             for k, v in zip(keys, combo):
-                assert lib.pg_set_tuning(k.encode(), v) == 0, (k, v)
+                e.set_tuning(k, v)
             ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             lib.pg_classify(e.h, w.mode, w.table_id, C.byref(soa), n, outs[i].data_ptr(), cptr, stream)  # warm
             ev0.record()

@@ -112,6 +112,17 @@ _SIGS = {
     "pg_create": (_P, [C.c_int]),
     "pg_destroy": (None, [_P]),
     "pg_set_tuning": (C.c_int, [C.c_char_p, C.c_int]),
+    "pg_ctx_set_tuning": (C.c_int, [_P, C.c_char_p, C.c_int]),
+    "pg_ctx_get_tuning": (C.c_int, [_P, C.c_char_p, C.POINTER(C.c_int)]),
+    "pg_ctx_device": (C.c_int, [_P]),
+    "pg_counters_snapshot": (C.c_int, [_P, C.POINTER(C.c_uint64), C.c_size_t]),
+    "pg_comm_unique_id": (C.c_int, [C.c_char_p]),
+    "pg_comm_init_rank": (C.c_int, [_P, C.c_int, C.c_char_p, C.c_int]),
+    "pg_comm_init_all": (C.c_int, [C.POINTER(_P), C.c_int]),
+    "pg_comm_destroy": (C.c_int, [_P]),
+    "pg_comm_rank": (C.c_int, [_P, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
+    "pg_allreduce_counters": (C.c_int, [_P, _P]),
+    "pg_allreduce_counters_all": (C.c_int, [C.POINTER(_P), C.c_int]),
     "pg_last_error": (C.c_char_p, [_P]),
     "pg_set_pod_if_name": (C.c_int, [_P, C.c_char_p, C.c_char_p, C.c_char_p]),
     "pg_set_host_interconnect_if_name": (C.c_int, [_P, C.c_char_p]),

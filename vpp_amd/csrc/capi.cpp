@@ -2,6 +2,7 @@
 // model, forwards to the renderer / engine and maps failures to PG_* codes + last_error.
 #include <cstring>
 #include <memory>
+#include <mutex>
 #include <stdexcept>
 
 #include "capi_internal.hpp"
@@ -91,6 +92,25 @@ int fail(pg_ctx* c, int code, const std::string& msg) {
     return code;
 }
 
+// Every entry point that touches the device makes the context's GPU current for the call and
+// restores the caller's afterwards: contexts on different GPUs can share a process, and a cgo
+// caller's goroutine may move between OS threads between two calls.
+struct DeviceGuard {
+    int prev = -1, dev = 0;
+    bool ok = true;
+    std::string err;
+    explicit DeviceGuard(const pg_ctx* c) : dev(c->eng.device) {
+        if (dev_get_device(&prev) != 0) prev = -1;
+        if (prev != dev) ok = dev_set_device(dev, &err) == 0;
+    }
+    ~DeviceGuard() {
+        if (prev >= 0 && prev != dev) (void)dev_set_device(prev, nullptr);
+    }
+};
+#define DEVICE_GUARD(ctx)                                             \
+    DeviceGuard guard_(ctx);                                          \
+    if (!guard_.ok) return fail(ctx, PG_EIO, "set device: " + guard_.err)
+
 std::string json_escape(const std::string& s) {
     std::string o;
     for (char ch : s) {
@@ -126,67 +146,47 @@ extern "C" {
 const char* pg_version(void) { return "policygpu 0.1 (gfx950)"; }
 
 pg_ctx* pg_create(int hip_device) {
+    if (hip_device < 0) return nullptr;
     auto* c = new (std::nothrow) pg_ctx();
     if (!c) return nullptr;
-    c->eng.device = hip_device;
-    std::string err;
-    if (dev_set_device(hip_device, &err) != 0) c->eng.last_error = err;
+    c->eng.device = hip_device;  // made current by every device-touching call (DeviceGuard)
     return c;
 }
 
-void pg_destroy(pg_ctx* ctx) { delete ctx; }
+void pg_destroy(pg_ctx* ctx) {
+    if (!ctx) return;
+    const Engine& E = ctx->eng;
+    if (E.cur || E.counters || E.comm || E.comm_check) {  // device resources: free them on their GPU
+        DeviceGuard g(ctx);
+        delete ctx;
+        return;
+    }
+    delete ctx;
+}
 
+// process defaults: contexts created afterwards start from them
 int pg_set_tuning(const char* key, int value) {
     if (!key) return PG_EINVAL;
-    if (std::string(key) == "root_bits_max") {  // applies to tables compiled afterwards
-        if (value < 4 || value > 16) return PG_EINVAL;
-        set_root_bits_max((uint32_t)value);
-        return PG_OK;
-    }
-    if (std::string(key) == "lc_dense12") {  // tables compiled afterwards
-        if (value < 1) return PG_EINVAL;
-        set_lc_dense12((uint32_t)value);
-        return PG_OK;
-    }
-    if (std::string(key) == "lc_max_stride") {  // tables compiled afterwards
-        if (value != 12 && value != 16 && value != 18) return PG_EINVAL;
-        set_lc_max_stride((uint32_t)value);
-        return PG_OK;
-    }
-    if (std::string(key) == "pair") {  // tables compiled afterwards
-        if (value < 0 || value > 2) return PG_EINVAL;
-        set_pair_enable((uint32_t)value);
-        return PG_OK;
-    }
-    if (std::string(key) == "lc_node") {  // tables compiled afterwards
-        if (value != 0 && value != 1) return PG_EINVAL;
-        set_lc_node((uint32_t)value);
-        return PG_OK;
-    }
-    if (std::string(key) == "lc_lds") {  // min blob words for the LC rebuild, 0 = off
-        if (value < 0) return PG_EINVAL;
-        set_lc_lds((uint32_t)value);
-        return PG_OK;
-    }
-    if (std::string(key) == "node_common") {  // common-row section of node images compiled afterwards
-        if (value != 0 && value != 1) return PG_EINVAL;
-        set_node_common((uint32_t)value);
-        return PG_OK;
-    }
-    if (std::string(key) == "node_build" || std::string(key) == "node_root_bits") {  // tables compiled afterwards
-        static uint32_t enable = 1, bits = 12;
-        if (std::string(key) == "node_build") {
-            if (value != 0 && value != 1) return PG_EINVAL;
-            enable = (uint32_t)value;
-        } else {
-            if (value < 4 || value > 16) return PG_EINVAL;
-            bits = (uint32_t)value;
-        }
-        set_node_tuning(enable, bits);
-        return PG_OK;
-    }
-    return dev_set_tuning(key, value) == 0 ? PG_OK : PG_EINVAL;
+    static std::mutex mu;
+    std::lock_guard<std::mutex> lk(mu);
+    return tuning_set(default_tuning(), key, value) == 0 ? PG_OK : PG_EINVAL;
 }
+
+int pg_ctx_set_tuning(pg_ctx* ctx, const char* key, int value) {
+    if (!ctx || !key) return PG_EINVAL;
+    bool compiler = false;
+    if (tuning_set(ctx->eng.tune, key, value, &compiler) != 0)
+        return fail(ctx, PG_EINVAL, std::string("bad tuning key or value: ") + key);
+    if (compiler) ctx->eng.touch();  // recompiled (and re-uploaded) on the next use
+    return PG_OK;
+}
+
+int pg_ctx_get_tuning(const pg_ctx* ctx, const char* key, int* value) {
+    if (!key || !value) return PG_EINVAL;
+    return tuning_get(ctx ? ctx->eng.tune : default_tuning(), key, value) == 0 ? PG_OK : PG_EINVAL;
+}
+
+int pg_ctx_device(const pg_ctx* ctx) { return ctx ? ctx->eng.device : PG_EINVAL; }
 
 const char* pg_last_error(const pg_ctx* ctx) { return ctx ? ctx->eng.last_error.c_str() : "null context"; }
 
@@ -384,6 +384,7 @@ int pg_interface_acls(pg_ctx* ctx, const char* if_name, char* inbound, size_t in
 
 int pg_sync_tables(pg_ctx* ctx) {
     if (!ctx) return PG_EINVAL;
+    DEVICE_GUARD(ctx);
     GUARD_BEGIN
     return ctx->eng.sync();
     GUARD_END(ctx)
@@ -638,6 +639,7 @@ int pg_node_common_stats(pg_ctx* ctx, uint64_t* base_image_bytes, uint64_t* comm
 int pg_classify(pg_ctx* ctx, int mode, int table_id, const pg_tuple_soa* t, uint64_t n, uint32_t* out,
                 uint64_t* counters, void* stream) {
     if (!ctx || !t || mode < 0 || mode > 2) return PG_EINVAL;
+    DEVICE_GUARD(ctx);
     GUARD_BEGIN
     int rc = ctx->eng.sync();
     if (rc) return rc;
@@ -649,8 +651,9 @@ int pg_classify(pg_ctx* ctx, int mode, int table_id, const pg_tuple_soa* t, uint
     if (!t->src_ip || !t->dst_ip || !t->dst_port || !t->proto || (mode == PG_MODE_CONN && !t->src_port))
         return fail(ctx, PG_EINVAL, "missing tuple field");
     std::string err;
-    if (dev_classify(T, mode, table_id, t->src_ip, t->dst_ip, t->src_port, t->dst_port, t->proto, n, out,
-                     (unsigned long long*)counters, stream, &err) != 0)
+    if (dev_classify(T, ctx->eng.tune, mode, table_id, t->src_ip, t->dst_ip, t->src_port, t->dst_port, t->proto, n,
+                     out, (unsigned long long*)counters, stream, &err) != 0 ||
+        dev_mark_use(ctx->eng.cur, stream, &err) != 0)
         return fail(ctx, PG_EIO, err);
     return PG_OK;
     GUARD_END(ctx)
@@ -658,25 +661,30 @@ int pg_classify(pg_ctx* ctx, int mode, int table_id, const pg_tuple_soa* t, uint
 
 int pg_classify_linear(pg_ctx* ctx, int table_id, const pg_tuple_soa* t, uint64_t n, uint32_t* out, void* stream) {
     if (!ctx || !t || !out) return PG_EINVAL;
+    DEVICE_GUARD(ctx);
     GUARD_BEGIN
     int rc = ctx->eng.sync();
     if (rc) return rc;
     const DevTableSet& T = *ctx->eng.view();
     if (table_id < 0 || (uint32_t)table_id >= T.n_tables) return fail(ctx, PG_EINVAL, "table id out of range");
     std::string err;
-    if (dev_classify_linear(T, table_id, t->src_ip, t->dst_ip, t->dst_port, t->proto, n, out, stream, &err) != 0)
+    if (dev_classify_linear(T, table_id, t->src_ip, t->dst_ip, t->dst_port, t->proto, n, out, stream, &err) != 0 ||
+        dev_mark_use(ctx->eng.cur, stream, &err) != 0)
         return fail(ctx, PG_EIO, err);
     return PG_OK;
     GUARD_END(ctx)
 }
 
 uint64_t* pg_counters_device(pg_ctx* ctx) {
-    if (!ctx || ctx->eng.sync() != PG_OK) return nullptr;
+    if (!ctx) return nullptr;
+    DeviceGuard g(ctx);
+    if (!g.ok || ctx->eng.sync() != PG_OK) return nullptr;
     return (uint64_t*)ctx->eng.counters;
 }
 
 int pg_reset_counters(pg_ctx* ctx, void* stream) {
     if (!ctx) return PG_EINVAL;
+    DEVICE_GUARD(ctx);
     int rc = ctx->eng.sync();
     if (rc) return rc;
     std::string err;
@@ -687,18 +695,167 @@ int pg_reset_counters(pg_ctx* ctx, void* stream) {
 
 int pg_read_counters(pg_ctx* ctx, uint64_t* host_out, size_t n) {
     if (!ctx || !host_out) return PG_EINVAL;
-    int rc = ctx->eng.sync();
+    DEVICE_GUARD(ctx);
+    Engine& E = ctx->eng;
+    int rc = E.sync();
     if (rc) return rc;
-    size_t k = std::min(n, ctx->eng.counter_slots);
     std::string err;
-    if (dev_sync(&err) != 0 || dev_copy_d2h(host_out, ctx->eng.counters, k * 8, &err) != 0)
+    E.snapshot.resize(E.counter_slots);
+    // the launches of this context that count have completed (their streams' events), then copy
+    if (dev_wait_uses(E.cur, &err) != 0 || dev_copy_d2h(E.snapshot.data(), E.counters, E.counter_slots * 8, &err) != 0)
         return fail(ctx, PG_EIO, err);
+    size_t k = std::min(n, E.counter_slots);
+    std::memcpy(host_out, E.snapshot.data(), k * 8);
     return (int)k;
+}
+
+int pg_counters_snapshot(const pg_ctx* ctx, uint64_t* host_out, size_t n) {
+    if (!ctx || (!host_out && n)) return PG_EINVAL;
+    const size_t k = std::min(n, ctx->eng.snapshot.size());
+    if (k) std::memcpy(host_out, ctx->eng.snapshot.data(), k * 8);
+    return (int)ctx->eng.snapshot.size();
+}
+
+// ---- RCCL: per-rule hit counters summed over GPUs --------------------------
+int pg_comm_unique_id(uint8_t* id) {
+    if (!id) return PG_EINVAL;
+    std::string err;
+    return dev_comm_unique_id(id, &err) == 0 ? PG_OK : PG_EIO;
+}
+
+static int comm_attach(pg_ctx* ctx, void* comm, int rank, int nranks) {
+    Engine& E = ctx->eng;
+    std::string err;
+    if (!E.comm_check && !(E.comm_check = (unsigned long long*)dev_alloc(4 * 8, &err)))
+        return fail(ctx, PG_ENOMEM, err);
+    if (E.comm) dev_comm_destroy(E.comm);
+    E.comm = comm;
+    E.comm_rank = rank;
+    E.comm_nranks = nranks;
+    return PG_OK;
+}
+
+int pg_comm_init_rank(pg_ctx* ctx, int nranks, const uint8_t* id, int rank) {
+    if (!ctx || !id || nranks < 1 || rank < 0 || rank >= nranks) return PG_EINVAL;
+    DEVICE_GUARD(ctx);
+    std::string err;
+    void* c = dev_comm_init_rank(nranks, id, rank, &err);
+    if (!c) return fail(ctx, PG_EIO, err);
+    return comm_attach(ctx, c, rank, nranks);
+}
+
+int pg_comm_init_all(pg_ctx* const* ctxs, int n) {
+    if (!ctxs || n < 1) return PG_EINVAL;
+    std::vector<int> devs(n);
+    for (int i = 0; i < n; i++) {
+        if (!ctxs[i]) return PG_EINVAL;
+        devs[i] = ctxs[i]->eng.device;
+    }
+    DeviceGuard g(ctxs[0]);
+    std::vector<void*> comms(n, nullptr);
+    std::string err;
+    if (dev_comm_init_all(comms.data(), devs.data(), n, &err) != 0) return fail(ctxs[0], PG_EIO, err);
+    for (int i = 0; i < n; i++) {
+        DeviceGuard gi(ctxs[i]);
+        int rc = gi.ok ? comm_attach(ctxs[i], comms[i], i, n) : fail(ctxs[i], PG_EIO, gi.err);
+        if (rc) {
+            for (int j = i + 1; j < n; j++) dev_comm_destroy(comms[j]);
+            return rc;
+        }
+    }
+    return PG_OK;
+}
+
+int pg_comm_destroy(pg_ctx* ctx) {
+    if (!ctx) return PG_EINVAL;
+    DEVICE_GUARD(ctx);
+    if (ctx->eng.comm) dev_comm_destroy(ctx->eng.comm);
+    ctx->eng.comm = nullptr;
+    ctx->eng.comm_rank = -1;
+    ctx->eng.comm_nranks = 0;
+    return PG_OK;
+}
+
+int pg_comm_rank(const pg_ctx* ctx, int* rank, int* nranks) {
+    if (!ctx) return PG_EINVAL;
+    if (rank) *rank = ctx->eng.comm_rank;
+    if (nranks) *nranks = ctx->eng.comm_nranks;
+    return ctx->eng.comm ? PG_OK : PG_ENOENT;
+}
+
+// The contexts' counters summed in place over their communicator (k = 1: this process's rank
+// of a multi-process communicator; k > 1: every context of one pg_comm_init_all group, in one
+// RCCL group call). First a max all-reduce of {slots, layout hash, ~slots, ~hash} proves that
+// every rank compiled the same counter layout (a mismatched all-reduce would hang or mix
+// slots); then ncclAllReduce(u64, sum). Synchronous; the host snapshots are refreshed.
+static int allreduce_counters(pg_ctx* const* ctxs, int k, void* const* streams) {
+    std::vector<void*> comms(k), sts(k);
+    std::vector<unsigned long long*> chk(k), bufs(k);
+    std::vector<int> devs(k);
+    std::string err;
+    for (int i = 0; i < k; i++) {
+        pg_ctx* c = ctxs[i];
+        if (!c) return PG_EINVAL;
+        Engine& E = c->eng;
+        if (!E.comm) return fail(c, PG_EINVAL, "no communicator (pg_comm_init_rank / pg_comm_init_all)");
+        if (k > 1 && E.comm_nranks != k) return fail(c, PG_EINVAL, "contexts are not one pg_comm_init_all group");
+        DeviceGuard g(c);
+        if (!g.ok) return fail(c, PG_EIO, g.err);
+        int rc = E.sync();
+        if (rc) return rc;
+        const uint64_t n = E.counter_slots, h = E.layout_hash;
+        const uint64_t v[4] = {n, h, ~n, ~h};
+        if (dev_wait_uses(E.cur, &err) != 0 || dev_copy_h2d(E.comm_check, v, sizeof v, &err) != 0)
+            return fail(c, PG_EIO, err);
+        comms[i] = E.comm, sts[i] = streams ? streams[i] : nullptr, chk[i] = E.comm_check;
+        bufs[i] = E.counters, devs[i] = E.device;
+    }
+    DeviceGuard g(ctxs[0]);
+    if (dev_comm_allreduce_u64(comms.data(), chk.data(), devs.data(), sts.data(), k, 4, true, &err) != 0)
+        return fail(ctxs[0], PG_EIO, err);
+    for (int i = 0; i < k; i++) {
+        Engine& E = ctxs[i]->eng;
+        uint64_t v[4];
+        if (dev_set_device(E.device, &err) != 0 || dev_stream_sync(sts[i], &err) != 0 ||
+            dev_copy_d2h(v, E.comm_check, sizeof v, &err) != 0)
+            return fail(ctxs[i], PG_EIO, err);
+        const uint64_t n = E.counter_slots, h = E.layout_hash;
+        if (v[0] != n || v[1] != h || v[2] != ~n || v[3] != ~h)
+            return fail(ctxs[i], PG_EFAULT, "ranks hold different counter layouts (tables differ): not reduced");
+    }
+    if (dev_comm_allreduce_u64(comms.data(), bufs.data(), devs.data(), sts.data(), k, ctxs[0]->eng.counter_slots,
+                               false, &err) != 0)
+        return fail(ctxs[0], PG_EIO, err);
+    for (int i = 0; i < k; i++) {
+        Engine& E = ctxs[i]->eng;
+        E.snapshot.resize(E.counter_slots);
+        if (dev_set_device(E.device, &err) != 0 || dev_stream_sync(sts[i], &err) != 0 ||
+            dev_copy_d2h(E.snapshot.data(), E.counters, E.counter_slots * 8, &err) != 0)
+            return fail(ctxs[i], PG_EIO, err);
+    }
+    return PG_OK;
+}
+
+int pg_allreduce_counters(pg_ctx* ctx, void* stream) {
+    if (!ctx) return PG_EINVAL;
+    GUARD_BEGIN
+    pg_ctx* c[1] = {ctx};
+    void* s[1] = {stream};
+    return allreduce_counters(c, 1, s);
+    GUARD_END(ctx)
+}
+
+int pg_allreduce_counters_all(pg_ctx* const* ctxs, int n) {
+    if (!ctxs || n < 1 || !ctxs[0]) return PG_EINVAL;
+    GUARD_BEGIN
+    return allreduce_counters(ctxs, n, nullptr);
+    GUARD_END(ctxs[0])
 }
 
 int pg_gen_tuples(pg_ctx* ctx, const pg_gen_spec* spec, uint64_t n, uint32_t* src, uint32_t* dst, uint16_t* sport,
                   uint16_t* dport, uint8_t* proto, void* stream) {
     if (!ctx || !spec || !src || !dst || !dport || !proto) return PG_EINVAL;
+    DEVICE_GUARD(ctx);
     GUARD_BEGIN
     int rc = ctx->eng.sync();
     if (rc) return rc;
@@ -726,7 +883,7 @@ int pg_gen_tuples(pg_ctx* ctx, const pg_gen_spec* spec, uint64_t n, uint32_t* sr
     g.n_port_pool = spec->port_pool ? spec->n_port_pool : 0;
     void *ipp = nullptr, *pp = nullptr, *zc = nullptr;
     auto cleanup = [&]() {
-        dev_sync(nullptr);
+        dev_stream_sync(stream, nullptr);  // k_gen has read the pools
         dev_release(ipp);
         dev_release(pp);
         dev_release(zc);
@@ -757,6 +914,7 @@ int pg_gen_tuples(pg_ctx* ctx, const pg_gen_spec* spec, uint64_t n, uint32_t* sr
 // Connection* preamble (aclengine_mock.go:273-420) on the host, testConnection on the device.
 int pg_connections(pg_ctx* ctx, const pg_conn_query* q, size_t n, int32_t* out, uint32_t* out_slot) {
     if (!ctx || (!q && n) || (!out && n)) return PG_EINVAL;
+    DEVICE_GUARD(ctx);
     GUARD_BEGIN
     Engine& E = ctx->eng;
     int rc = E.sync();

@@ -17,10 +17,13 @@
 // Semantics of one evaluation == evalACL (aclengine_mock.go:503-652) over the ACL the table
 // was compiled from (engine.cpp compile_acl_rule); the output word packs the ACLAction (or
 // ConnAction) in bits 31-30 and the deciding counter slot in bits 29-0.
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <cstring>
+#include <utility>
 
 #include "classify.hpp"
 
@@ -40,6 +43,10 @@ struct DeviceBuffers {
     DevTableSet view{};
     std::vector<DevTable> host_tabs;
     std::vector<uint32_t> host_blob_words;
+    // streams that launched kernels reading this set, with an event recorded after the last
+    // launch on each: the set is freed (and counters read) once those have completed, without
+    // a device-wide synchronisation
+    std::vector<std::pair<hipStream_t, hipEvent_t>> uses;
 };
 
 const DevTableSet& dev_view(const DeviceBuffers* b) { return b->view; }
@@ -48,6 +55,7 @@ int dev_set_device(int dev, std::string* err) {
     HIPCHK(hipSetDevice(dev));
     return 0;
 }
+int dev_get_device(int* dev) { return hipGetDevice(dev) == hipSuccess ? 0 : -1; }
 void* dev_alloc(size_t bytes, std::string* err) {
     void* p = nullptr;
     hipError_t e = hipMalloc(&p, bytes ? bytes : 16);
@@ -74,6 +82,29 @@ int dev_copy_h2d(void* dst, const void* src, size_t bytes, std::string* err) {
 }
 int dev_sync(std::string* err) {
     HIPCHK(hipDeviceSynchronize());
+    return 0;
+}
+int dev_stream_sync(void* stream, std::string* err) {
+    HIPCHK(hipStreamSynchronize((hipStream_t)stream));
+    return 0;
+}
+
+int dev_mark_use(DeviceBuffers* b, void* stream, std::string* err) {
+    const hipStream_t s = (hipStream_t)stream;
+    for (auto& u : b->uses)
+        if (u.first == s) {
+            HIPCHK(hipEventRecord(u.second, s));
+            return 0;
+        }
+    hipEvent_t e;
+    HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    b->uses.push_back({s, e});
+    HIPCHK(hipEventRecord(e, s));
+    return 0;
+}
+
+int dev_wait_uses(DeviceBuffers* b, std::string* err) {
+    for (auto& u : b->uses) HIPCHK(hipEventSynchronize(u.second));
     return 0;
 }
 
@@ -110,7 +141,7 @@ DeviceBuffers* dev_upload(const HostTableSet& h, std::string* err) {
         delete b;
         return nullptr;
     }
-    if (dev_copy_h2d(b->blob, img.data(), off, err) != 0 || dev_sync(err) != 0) {
+    if (dev_copy_h2d(b->blob, img.data(), off, err) != 0) {  // synchronous: the copy has landed
         dev_release(b->blob);
         delete b;
         return nullptr;
@@ -144,9 +175,125 @@ DeviceBuffers* dev_upload(const HostTableSet& h, std::string* err) {
 
 void dev_free(DeviceBuffers* b) {
     if (!b) return;
-    (void)hipDeviceSynchronize();
+    for (auto& u : b->uses) {  // launches that read the set have completed
+        (void)hipEventSynchronize(u.second);
+        (void)hipEventDestroy(u.second);
+    }
     dev_release(b->blob);
     delete b;
+}
+
+// ---- RCCL (counter all-reduce) ------------------------------------------------
+// librccl is opened at first use (dlopen of the SONAME: a process that already holds one --
+// e.g. torch's -- shares it), so contexts that never all-reduce need no RCCL.
+namespace {
+struct Rccl {
+    decltype(&ncclGetUniqueId) get_id = nullptr;
+    decltype(&ncclCommInitRank) init_rank = nullptr;
+    decltype(&ncclCommInitAll) init_all = nullptr;
+    decltype(&ncclAllReduce) all_reduce = nullptr;
+    decltype(&ncclGroupStart) group_start = nullptr;
+    decltype(&ncclGroupEnd) group_end = nullptr;
+    decltype(&ncclCommDestroy) destroy = nullptr;
+    decltype(&ncclGetErrorString) errstr = nullptr;
+    std::string load_error;
+};
+const Rccl& rccl() {
+    static const Rccl r = [] {
+        Rccl x;
+        void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+        if (!h) h = dlopen("librccl.so", RTLD_NOW | RTLD_GLOBAL);
+        if (!h) {
+            const char* e = dlerror();
+            x.load_error = std::string("dlopen librccl: ") + (e ? e : "?");
+            return x;
+        }
+        auto sym = [&](auto& f, const char* name) { f = reinterpret_cast<std::decay_t<decltype(f)>>(dlsym(h, name)); };
+        sym(x.get_id, "ncclGetUniqueId");
+        sym(x.init_rank, "ncclCommInitRank");
+        sym(x.init_all, "ncclCommInitAll");
+        sym(x.all_reduce, "ncclAllReduce");
+        sym(x.group_start, "ncclGroupStart");
+        sym(x.group_end, "ncclGroupEnd");
+        sym(x.destroy, "ncclCommDestroy");
+        sym(x.errstr, "ncclGetErrorString");
+        if (!x.get_id || !x.init_rank || !x.init_all || !x.all_reduce || !x.group_start || !x.group_end ||
+            !x.destroy || !x.errstr)
+            x.load_error = "librccl: missing symbols";
+        return x;
+    }();
+    return r;
+}
+bool rccl_ok(std::string* err) {
+    if (!rccl().load_error.empty()) {
+        if (err) *err = rccl().load_error;
+        return false;
+    }
+    return true;
+}
+}  // namespace
+
+#define NCCLCHK(expr)                                                               \
+    do {                                                                            \
+        ncclResult_t r_ = (expr);                                                   \
+        if (r_ != ncclSuccess) {                                                    \
+            if (err) *err = std::string(#expr ": ") + rccl().errstr(r_);            \
+            return -1;                                                              \
+        }                                                                           \
+    } while (0)
+
+int dev_comm_unique_id(uint8_t* id, std::string* err) {
+    if (!rccl_ok(err)) return -1;
+    ncclUniqueId u;
+    NCCLCHK(rccl().get_id(&u));
+    std::memcpy(id, u.internal, sizeof(u.internal));
+    return 0;
+}
+
+void* dev_comm_init_rank(int nranks, const uint8_t* id, int rank, std::string* err) {
+    if (!rccl_ok(err)) return nullptr;
+    ncclUniqueId u;
+    std::memcpy(u.internal, id, sizeof(u.internal));
+    ncclComm_t c = nullptr;
+    const ncclResult_t r = rccl().init_rank(&c, nranks, u, rank);
+    if (r != ncclSuccess) {
+        if (err) *err = std::string("ncclCommInitRank: ") + rccl().errstr(r);
+        return nullptr;
+    }
+    return c;
+}
+
+int dev_comm_init_all(void** comms, const int* devs, int n, std::string* err) {
+    if (!rccl_ok(err)) return -1;
+    std::vector<ncclComm_t> c(n, nullptr);
+    NCCLCHK(rccl().init_all(c.data(), n, devs));
+    for (int i = 0; i < n; i++) comms[i] = c[i];
+    return 0;
+}
+
+void dev_comm_destroy(void* comm) {
+    if (comm && rccl().destroy) (void)rccl().destroy((ncclComm_t)comm);
+}
+
+// In-place ncclAllReduce of k buffers (one per communicator of a group; k = 1 for one rank of
+// a multi-process communicator), u64 max or sum, on the given streams; devs[i] is made current
+// around each call (the caller restores its device).
+int dev_comm_allreduce_u64(void* const* comms, unsigned long long* const* bufs, const int* devs,
+                           void* const* streams, int k, size_t count, bool max, std::string* err) {
+    if (!rccl_ok(err)) return -1;
+    if (k > 1) NCCLCHK(rccl().group_start());
+    for (int i = 0; i < k; i++) {
+        HIPCHK(hipSetDevice(devs[i]));
+        const ncclResult_t r = rccl().all_reduce(bufs[i], bufs[i], count, ncclUint64, max ? ncclMax : ncclSum,
+                                                 (ncclComm_t)comms[i], (hipStream_t)streams[i]);
+        if (r != ncclSuccess) {
+            if (k > 1) (void)rccl().group_end();
+            if (err) *err = std::string("ncclAllReduce: ") + rccl().errstr(r);
+            return -1;
+        }
+    }
+    if (k > 1) NCCLCHK(rccl().group_end());
+    return 0;
 }
 
 constexpr int kBlock = 256;
@@ -501,46 +648,30 @@ __global__ void k_conn_queries(DevTableSet T, const ConnQueryDev* q, uint32_t n,
 }
 
 // ---- launchers --------------------------------------------------------------------------------
-static uint32_t g_blocks_per_cu = 0;        // 0: as many workgroups per CU as fit (occupancy)
-static uint32_t g_stage_max_words = kStageBlobWords;  // blobs up to 64 KiB are staged in LDS
-static uint32_t g_node_stage_max_words = 16384;  // node images up to 64 KiB are staged in LDS
-static uint32_t g_stage_root_max_words = 16400;  // larger blobs: header + src root up to 2^14 entries
-static uint32_t g_node_path = 1;            // PERPOD / CONN through the node classifier when built
-// LDS bytes (image + counter histogram) up to which a node image's common-row section is staged
-// and used: 80 KiB keeps two 512-thread workgroups per CU
-static size_t g_node_common_lds_max = 80u << 10;
+// Launch knobs come from the calling context's Tuning (device.hpp): blocks_per_cu (0 = as many
+// workgroups per CU as fit), stage_max_words (blobs up to 64 KiB staged in LDS),
+// node_stage_max_words, stage_root_max_words (larger blobs: header + src root up to 2^14
+// entries), node_path, node_common_lds_max (LDS bytes -- image + counter histogram -- up to
+// which a node image's common-row section is staged: 80 KiB keeps two 512-thread workgroups
+// per CU), block_stage (workgroup size of LDS-staged launches; 0 = per mode).
 constexpr uint32_t kCommonStageExtraWords = 8192;  // the section may take the image past the base cap
-// workgroup size of LDS-staged classify launches; 0 = per mode (SINGLE 1024, SINGLE with
-// counters and PERPOD / CONN 512: tools/sweep.py on MI355X)
-static uint32_t g_block_stage = 0;
 
-int dev_set_tuning(const std::string& key, int value) {
-    if (key == "blocks_per_cu" && value >= 0 && value <= 64) g_blocks_per_cu = (uint32_t)value;
-    else if (key == "stage_max_words" && value >= 0 && value <= 36864) g_stage_max_words = (uint32_t)value;
-    else if (key == "node_stage_max_words" && value >= 0 && value <= 36864) g_node_stage_max_words = (uint32_t)value;
-    else if (key == "stage_root_max_words" && value >= 0 && value <= 36864) g_stage_root_max_words = (uint32_t)value;
-    else if (key == "node_path" && (value == 0 || value == 1)) g_node_path = (uint32_t)value;
-    else if (key == "node_common_lds_max" && value >= 0 && value <= (160 << 10)) g_node_common_lds_max = (size_t)value;
-    else if (key == "block_stage" && (value == 0 || value == 256 || value == 512 || value == 1024))
-        g_block_stage = (uint32_t)value;
-    else return -1;
-    return 0;
-}
-
+// CUs of the current device (per device: contexts on different GPUs share the process)
 static uint32_t num_cus() {
-    static int cached_dev = -1;
-    static uint32_t cus = 256;
+    constexpr int kMaxDev = 64;
+    static uint32_t cus[kMaxDev] = {};
     int dev = 0;
-    if (hipGetDevice(&dev) == hipSuccess && dev != cached_dev) {
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDev) return 256;
+    if (!cus[dev]) {
         hipDeviceProp_t p;
-        if (hipGetDeviceProperties(&p, dev) == hipSuccess && p.multiProcessorCount > 0) cus = p.multiProcessorCount;
-        cached_dev = dev;
+        cus[dev] = (hipGetDeviceProperties(&p, dev) == hipSuccess && p.multiProcessorCount > 0)
+                       ? (uint32_t)p.multiProcessorCount : 256u;
     }
-    return cus;
+    return cus[dev];
 }
 
-static int grid_for(uint64_t items) {
-    const uint32_t bpc = g_blocks_per_cu ? g_blocks_per_cu : 4u;
+static int grid_for(uint64_t items, uint32_t blocks_per_cu = 0) {
+    const uint32_t bpc = blocks_per_cu ? blocks_per_cu : 4u;
     uint64_t g = (items + kBlock - 1) / kBlock;
     return (int)std::max<uint64_t>(1, std::min<uint64_t>(g, (uint64_t)num_cus() * bpc));
 }
@@ -549,49 +680,49 @@ static int grid_for(uint64_t items) {
 // (registers / LDS of this instantiation), so no workgroup waits for another to finish, capped
 // by the work and by blocks_per_cu when set.
 template <class K>
-static int grid_resident(K kernel, int bs, size_t lds, uint64_t items) {
+static int grid_resident(K kernel, int bs, size_t lds, uint64_t items, uint32_t blocks_per_cu) {
     int per_cu = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, bs, lds) != hipSuccess || per_cu < 1)
         per_cu = 1;
-    if (g_blocks_per_cu) per_cu = std::min<int>(per_cu, (int)g_blocks_per_cu);
+    if (blocks_per_cu) per_cu = std::min<int>(per_cu, (int)blocks_per_cu);
     const uint64_t g = (items + bs - 1) / bs;
     return (int)std::max<uint64_t>(1, std::min<uint64_t>(g, (uint64_t)num_cus() * per_cu));
 }
 
 template <int MODE, bool COUNT, bool VEC, int STAGE, bool NODE, int BS>
-static void launch_bs(const DevTableSet& T, int t, const uint32_t* src, const uint32_t* dst, const uint16_t* sport,
+static void launch_bs(const DevTableSet& T, const Tuning& tu, int t, const uint32_t* src, const uint32_t* dst, const uint16_t* sport,
                       const uint16_t* dport, const uint8_t* proto, uint64_t n, uint32_t* out,
                       unsigned long long* counters, hipStream_t st, size_t hist, uint32_t stage, uint64_t items) {
     auto k = k_classify<MODE, COUNT, VEC, STAGE, NODE, BS>;
     const size_t lds = hist + (size_t)stage * 4;
-    hipLaunchKernelGGL(k, dim3(grid_resident(k, BS, lds, items)), dim3(BS), lds, st, T, t, src, dst, sport, dport,
+    hipLaunchKernelGGL(k, dim3(grid_resident(k, BS, lds, items, tu.blocks_per_cu)), dim3(BS), lds, st, T, t, src, dst, sport, dport,
                        proto, n, out, counters, stage);
 }
 
 // Workgroup size: a staged image is shared by the workgroup, so larger workgroups hold more
 // waves per CU for the same LDS.
 template <int MODE, bool COUNT, bool VEC, int STAGE, bool NODE>
-static void launch_one(const DevTableSet& T, int t, const uint32_t* src, const uint32_t* dst, const uint16_t* sport,
+static void launch_one(const DevTableSet& T, const Tuning& tu, int t, const uint32_t* src, const uint32_t* dst, const uint16_t* sport,
                        const uint16_t* dport, const uint8_t* proto, uint64_t n, uint32_t* out,
                        unsigned long long* counters, hipStream_t st, size_t hist, uint32_t stage, uint64_t items) {
     if constexpr (STAGE) {
         // 512 (A/B on MI355X: SINGLE with counters +14 % over 1024 at config 2; without
         // counters +2.5 % since SINGLE classifies one tuple per chunk, v15), except SINGLE
         // without counters over an HBM blob with its root staged: 1024 (config 4 +1.3 %)
-        const uint32_t bs = g_block_stage ? g_block_stage : (MODE == 0 && !COUNT && STAGE == 2 ? 1024u : 512u);
+        const uint32_t bs = tu.block_stage ? tu.block_stage : (MODE == 0 && !COUNT && STAGE == 2 ? 1024u : 512u);
         if (bs == 1024u)
-            return launch_bs<MODE, COUNT, VEC, STAGE, NODE, 1024>(T, t, src, dst, sport, dport, proto, n, out, counters,
-                                                                  st, hist, stage, items);
+            return launch_bs<MODE, COUNT, VEC, STAGE, NODE, 1024>(T, tu, t, src, dst, sport, dport, proto, n, out,
+                                                                  counters, st, hist, stage, items);
         if (bs == 512u)
-            return launch_bs<MODE, COUNT, VEC, STAGE, NODE, 512>(T, t, src, dst, sport, dport, proto, n, out, counters,
-                                                                 st, hist, stage, items);
+            return launch_bs<MODE, COUNT, VEC, STAGE, NODE, 512>(T, tu, t, src, dst, sport, dport, proto, n, out,
+                                                                 counters, st, hist, stage, items);
     }
-    launch_bs<MODE, COUNT, VEC, STAGE, NODE, 256>(T, t, src, dst, sport, dport, proto, n, out, counters, st, hist, stage,
-                                                  items);
+    launch_bs<MODE, COUNT, VEC, STAGE, NODE, 256>(T, tu, t, src, dst, sport, dport, proto, n, out, counters, st, hist,
+                                                  stage, items);
 }
 
 template <int MODE, bool COUNT, bool VEC>
-static void launch_classify(const DevTableSet& T, int t, const uint32_t* src, const uint32_t* dst,
+static void launch_classify(const DevTableSet& T, const Tuning& tu, int t, const uint32_t* src, const uint32_t* dst,
                             const uint16_t* sport, const uint16_t* dport, const uint8_t* proto, uint64_t n,
                             uint32_t* out, unsigned long long* counters, hipStream_t st) {
     const size_t hist = (COUNT && T.n_slots <= kLdsHistMax) ? T.n_slots * 4 : 0;
@@ -600,50 +731,50 @@ static void launch_classify(const DevTableSet& T, int t, const uint32_t* src, co
         const DevTable& hd = T.host_tabs[t];
         const uint32_t words = T.host_blob_words[t];
         const uint32_t root_words = (kSrcRoot + (1u << ((hd.fsk >> 8) & 0xFFu)) + 3u) & ~3u;
-        if (!(hd.fsk & kFlagLinear) && words && words <= g_stage_max_words)
-            launch_one<MODE, COUNT, VEC, 1, false>(T, t, src, dst, sport, dport, proto, n, out, counters, st, hist,
+        if (!(hd.fsk & kFlagLinear) && words && words <= tu.stage_max_words)
+            launch_one<MODE, COUNT, VEC, 1, false>(T, tu, t, src, dst, sport, dport, proto, n, out, counters, st, hist,
                                                    words, items);
-        else if (!(hd.fsk & kFlagLinear) && words && root_words <= g_stage_root_max_words)
-            launch_one<MODE, COUNT, VEC, 2, false>(T, t, src, dst, sport, dport, proto, n, out, counters, st, hist,
+        else if (!(hd.fsk & kFlagLinear) && words && root_words <= tu.stage_root_max_words)
+            launch_one<MODE, COUNT, VEC, 2, false>(T, tu, t, src, dst, sport, dport, proto, n, out, counters, st, hist,
                                                    root_words, items);
         else
-            launch_one<MODE, COUNT, VEC, 0, false>(T, t, src, dst, sport, dport, proto, n, out, counters, st, hist,
+            launch_one<MODE, COUNT, VEC, 0, false>(T, tu, t, src, dst, sport, dport, proto, n, out, counters, st, hist,
                                                    0, items);
-    } else if (g_node_path && T.node.img) {
+    } else if (tu.node_path && T.node.img) {
         // the image with its common-row section when that fits the LDS budget next to the
         // histogram, else the base image (STAGE 1), else the image is read from HBM / L2
-        if (T.node.cmap && hist + (size_t)T.node.img_words * 4 <= g_node_common_lds_max &&
-            T.node.img_words <= g_node_stage_max_words + kCommonStageExtraWords)
-            launch_one<MODE, COUNT, VEC, 3, true>(T, t, src, dst, sport, dport, proto, n, out, counters, st, hist,
+        if (T.node.cmap && hist + (size_t)T.node.img_words * 4 <= tu.node_common_lds_max &&
+            T.node.img_words <= tu.node_stage_max_words + kCommonStageExtraWords)
+            launch_one<MODE, COUNT, VEC, 3, true>(T, tu, t, src, dst, sport, dport, proto, n, out, counters, st, hist,
                                                   T.node.img_words, items);
-        else if (T.node.img_words_base <= g_node_stage_max_words)
-            launch_one<MODE, COUNT, VEC, 1, true>(T, t, src, dst, sport, dport, proto, n, out, counters, st, hist,
+        else if (T.node.img_words_base <= tu.node_stage_max_words)
+            launch_one<MODE, COUNT, VEC, 1, true>(T, tu, t, src, dst, sport, dport, proto, n, out, counters, st, hist,
                                                   T.node.img_words_base, items);
         else
-            launch_one<MODE, COUNT, VEC, 0, true>(T, t, src, dst, sport, dport, proto, n, out, counters, st, hist,
+            launch_one<MODE, COUNT, VEC, 0, true>(T, tu, t, src, dst, sport, dport, proto, n, out, counters, st, hist,
                                                   0, items);
     } else {
-        launch_one<MODE, COUNT, VEC, 0, false>(T, t, src, dst, sport, dport, proto, n, out, counters, st, hist, 0,
+        launch_one<MODE, COUNT, VEC, 0, false>(T, tu, t, src, dst, sport, dport, proto, n, out, counters, st, hist, 0,
                                                items);
     }
 }
 
 template <int MODE>
-static void dispatch_mode(bool count, bool vec, const DevTableSet& T, int t, const uint32_t* src,
+static void dispatch_mode(bool count, bool vec, const DevTableSet& T, const Tuning& tu, int t, const uint32_t* src,
                           const uint32_t* dst, const uint16_t* sport, const uint16_t* dport, const uint8_t* proto,
                           uint64_t n, uint32_t* out, unsigned long long* counters, hipStream_t st) {
     if (count) {
-        if (vec) launch_classify<MODE, true, true>(T, t, src, dst, sport, dport, proto, n, out, counters, st);
-        else launch_classify<MODE, true, false>(T, t, src, dst, sport, dport, proto, n, out, counters, st);
+        if (vec) launch_classify<MODE, true, true>(T, tu, t, src, dst, sport, dport, proto, n, out, counters, st);
+        else launch_classify<MODE, true, false>(T, tu, t, src, dst, sport, dport, proto, n, out, counters, st);
     } else {
-        if (vec) launch_classify<MODE, false, true>(T, t, src, dst, sport, dport, proto, n, out, counters, st);
-        else launch_classify<MODE, false, false>(T, t, src, dst, sport, dport, proto, n, out, counters, st);
+        if (vec) launch_classify<MODE, false, true>(T, tu, t, src, dst, sport, dport, proto, n, out, counters, st);
+        else launch_classify<MODE, false, false>(T, tu, t, src, dst, sport, dport, proto, n, out, counters, st);
     }
 }
 
-int dev_classify(const DevTableSet& T, int mode, int table_id, const uint32_t* src, const uint32_t* dst,
-                 const uint16_t* sport, const uint16_t* dport, const uint8_t* proto, uint64_t n, uint32_t* out,
-                 unsigned long long* counters, void* stream, std::string* err) {
+int dev_classify(const DevTableSet& T, const Tuning& tu, int mode, int table_id, const uint32_t* src,
+                 const uint32_t* dst, const uint16_t* sport, const uint16_t* dport, const uint8_t* proto, uint64_t n,
+                 uint32_t* out, unsigned long long* counters, void* stream, std::string* err) {
     if (n == 0) return 0;
     auto al = [](const void* p, uintptr_t a) { return ((uintptr_t)p & (a - 1)) == 0; };
     // the group loads: 4*P-byte src/dst/out (16-B pieces), 2*P-byte ports, P-byte protocols
@@ -652,9 +783,9 @@ int dev_classify(const DevTableSet& T, int mode, int table_id, const uint32_t* s
                      (mode != 2 || al(sport, kPort));
     hipStream_t st = (hipStream_t)stream;
     const bool count = counters != nullptr;
-    if (mode == 0) dispatch_mode<0>(count, vec, T, table_id, src, dst, sport, dport, proto, n, out, counters, st);
-    else if (mode == 1) dispatch_mode<1>(count, vec, T, table_id, src, dst, sport, dport, proto, n, out, counters, st);
-    else dispatch_mode<2>(count, vec, T, table_id, src, dst, sport, dport, proto, n, out, counters, st);
+    if (mode == 0) dispatch_mode<0>(count, vec, T, tu, table_id, src, dst, sport, dport, proto, n, out, counters, st);
+    else if (mode == 1) dispatch_mode<1>(count, vec, T, tu, table_id, src, dst, sport, dport, proto, n, out, counters, st);
+    else dispatch_mode<2>(count, vec, T, tu, table_id, src, dst, sport, dport, proto, n, out, counters, st);
     HIPCHK(hipGetLastError());
     return 0;
 }

@@ -101,16 +101,46 @@ struct HostTableSet {
     DevNode node{};                              // header fields (pointers unset)
 };
 
-// fastpath.cpp: classification blob of one table (false = does not fit the budgets). When
-// `an` is given it receives the table's class analysis for build_node.
-struct TableAnalysis;
 // table blobs up to this many words are staged in LDS by default (64 KiB); larger ones are
 // read from HBM and compiled with level-compressed tries
 constexpr uint32_t kStageBlobWords = 16384;
+
+// Knobs of one engine context (pg_ctx_set_tuning; pg_set_tuning sets the process defaults new
+// contexts start from). Compiler knobs apply to the tables the context compiles next; launch
+// knobs to its next launches. Keys and ranges: tuning_set (engine.cpp), include/policygpu.h.
+struct Tuning {
+    // table compiler
+    uint32_t root_bits_max = 16;   // cap of the tries' root stride (4..16)
+    uint32_t lc_lds = 4096;        // LC rebuild of LDS-sized blobs of at least this many words (0 = off)
+    uint32_t lc_dense12 = 16;      // boundaries in a child's span that earn it a 12-bit stride
+    uint32_t lc_max_stride = 16;   // widest level-compressed stride (12, 16, 18)
+    uint32_t pair = 1;             // PAIR for tables CROSS cannot take (0 = CAND, 2 = wherever it fits)
+    uint32_t node_build = 1;       // build the node classifier (PERPOD / CONN)
+    uint32_t node_root_bits = 12;  // its IPv4 / key trie root stride cap (4..16)
+    uint32_t lc_node = 0;          // level-compressed node IPv4 trie
+    uint32_t node_common = 1;      // common-row section of node images
+    // launches
+    uint32_t blocks_per_cu = 0;    // cap on resident workgroups per CU (0 = occupancy)
+    uint32_t stage_max_words = kStageBlobWords;  // table blobs staged whole in LDS
+    uint32_t node_stage_max_words = 16384;       // node images staged in LDS
+    uint32_t stage_root_max_words = 16400;       // larger blobs: header + src root up to 2^14 entries
+    uint32_t node_path = 1;        // PERPOD / CONN through the node classifier when built
+    uint32_t node_common_lds_max = 80u << 10;    // LDS bytes up to which the common-row section is staged
+    uint32_t block_stage = 0;      // workgroup size of LDS-staged launches (0 = per mode)
+};
+// key -> field; 0 ok, -1 unknown key or value out of range. *compiler: the key changes how
+// tables are compiled (the context recompiles on its next use).
+int tuning_set(Tuning& t, const std::string& key, int value, bool* compiler = nullptr);
+int tuning_get(const Tuning& t, const std::string& key, int* value);
+Tuning& default_tuning();  // process defaults (contexts copy them when created)
+
+// fastpath.cpp: classification blob of one table (false = does not fit the budgets). When
+// `an` is given it receives the table's class analysis for build_node.
+struct TableAnalysis;
 // lc: level-compressed tries (wider strides in dense subtrees) for blobs read from HBM
 bool build_fast_table(const DevRule* rules, uint32_t n, uint32_t rule_base, uint32_t default_slot,
-                      std::vector<uint32_t>& blob, uint64_t cross_budget, TableAnalysis** an = nullptr,
-                      bool lc = false);
+                      std::vector<uint32_t>& blob, uint64_t cross_budget, const Tuning& tu,
+                      TableAnalysis** an = nullptr, bool lc = false);
 void free_analysis(TableAnalysis* an);
 // fastpath.cpp: the node classifier over the tables with an analysis (null = not covered).
 // pods: {IPv4, interface, inbound table, outbound table} of local pods; node_end: the same for
@@ -120,15 +150,7 @@ struct NodePod {
     int32_t ifc, tin, tout;
 };
 bool build_node(HostTableSet& h, const std::vector<TableAnalysis*>& an, const std::vector<NodePod>& pods,
-                const NodePod& node_end);
-void set_root_bits_max(uint32_t bits);  // cap of the tries' root stride (4..16)
-void set_node_tuning(uint32_t enable, uint32_t root_bits);
-void set_node_common(uint32_t on);  // common-row section of the node image (images compiled afterwards)
-void set_pair_enable(uint32_t on);  // PAIR mode for tables CROSS cannot take (tables compiled afterwards)
-void set_lc_node(uint32_t on);  // level-compressed node IPv4 trie (tables compiled afterwards)
-void set_lc_lds(uint32_t on);
-void set_lc_max_stride(uint32_t s);  // widest level-compressed stride (12, 16 or 18; default 16)
-void set_lc_dense12(uint32_t n);  // level-compression threshold for 12-bit strides (default 256)   // level-compressed tries also for LDS-staged blobs that stay <= 64 KiB
+                const NodePod& node_end, const Tuning& tu);
 
 struct GenParams {         // device view of pg_gen_spec
     uint64_t seed, index_base;
@@ -154,9 +176,9 @@ DeviceBuffers* dev_upload(const HostTableSet& h, std::string* err);
 void dev_free(DeviceBuffers* b);
 const DevTableSet& dev_view(const DeviceBuffers* b);
 
-int dev_classify(const DevTableSet& T, int mode, int table_id, const uint32_t* src, const uint32_t* dst,
-                 const uint16_t* sport, const uint16_t* dport, const uint8_t* proto, uint64_t n, uint32_t* out,
-                 unsigned long long* counters, void* stream, std::string* err);
+int dev_classify(const DevTableSet& T, const Tuning& tu, int mode, int table_id, const uint32_t* src,
+                 const uint32_t* dst, const uint16_t* sport, const uint16_t* dport, const uint8_t* proto, uint64_t n,
+                 uint32_t* out, unsigned long long* counters, void* stream, std::string* err);
 int dev_classify_linear(const DevTableSet& T, int table_id, const uint32_t* src, const uint32_t* dst,
                         const uint16_t* dport, const uint8_t* proto, uint64_t n, uint32_t* out, void* stream,
                         std::string* err);
@@ -165,12 +187,23 @@ int dev_gen(const DevTableSet& T, const GenParams& g, uint64_t n, uint32_t* src,
 int dev_conn_queries(const DevTableSet& T, const ConnQueryDev* q_host, size_t n, uint32_t* out_host,
                      std::string* err);
 int dev_set_device(int dev, std::string* err);
-int dev_set_tuning(const std::string& key, int value);
+int dev_get_device(int* dev);
 void* dev_alloc(size_t bytes, std::string* err);
 void dev_release(void* p);
 int dev_memset(void* p, int v, size_t bytes, void* stream, std::string* err);
 int dev_copy_d2h(void* dst, const void* src, size_t bytes, std::string* err);
 int dev_copy_h2d(void* dst, const void* src, size_t bytes, std::string* err);
 int dev_sync(std::string* err);
+int dev_stream_sync(void* stream, std::string* err);
+// record that `stream` launched kernels reading table set b (dev_free / dev_wait_uses wait for them)
+int dev_mark_use(DeviceBuffers* b, void* stream, std::string* err);
+int dev_wait_uses(DeviceBuffers* b, std::string* err);
+// RCCL communicators (opaque ncclComm_t), librccl opened on first use
+int dev_comm_unique_id(uint8_t* id /* 128 B */, std::string* err);
+void* dev_comm_init_rank(int nranks, const uint8_t* id, int rank, std::string* err);
+int dev_comm_init_all(void** comms, const int* devs, int n, std::string* err);
+void dev_comm_destroy(void* comm);
+int dev_comm_allreduce_u64(void* const* comms, unsigned long long* const* bufs, const int* devs,
+                           void* const* streams, int k, size_t count, bool max, std::string* err);
 
 }  // namespace pg

@@ -10,8 +10,64 @@
 
 namespace pg {
 
-uint32_t g_lc_lds = 4096;  // LC rebuild of LDS-sized blobs of at least this many words (0 = off)
-void set_lc_lds(uint32_t on) { g_lc_lds = on; }
+// ---- tuning --------------------------------------------------------------------------------
+Tuning& default_tuning() {
+    static Tuning t;
+    return t;
+}
+
+namespace {
+struct Knob {
+    const char* key;
+    uint32_t Tuning::*field;
+    int lo, hi;
+    bool compiler;
+    bool allowed(int v) const;
+};
+const Knob kKnobs[] = {
+    {"root_bits_max", &Tuning::root_bits_max, 4, 16, true},
+    {"lc_lds", &Tuning::lc_lds, 0, 1 << 30, true},
+    {"lc_dense12", &Tuning::lc_dense12, 1, 1 << 30, true},
+    {"lc_max_stride", &Tuning::lc_max_stride, 12, 18, true},
+    {"pair", &Tuning::pair, 0, 2, true},
+    {"node_build", &Tuning::node_build, 0, 1, true},
+    {"node_root_bits", &Tuning::node_root_bits, 4, 16, true},
+    {"lc_node", &Tuning::lc_node, 0, 1, true},
+    {"node_common", &Tuning::node_common, 0, 1, true},
+    {"blocks_per_cu", &Tuning::blocks_per_cu, 0, 64, false},
+    {"stage_max_words", &Tuning::stage_max_words, 0, 36864, false},
+    {"node_stage_max_words", &Tuning::node_stage_max_words, 0, 36864, false},
+    {"stage_root_max_words", &Tuning::stage_root_max_words, 0, 36864, false},
+    {"node_path", &Tuning::node_path, 0, 1, false},
+    {"node_common_lds_max", &Tuning::node_common_lds_max, 0, 160 << 10, false},
+    {"block_stage", &Tuning::block_stage, 0, 1024, false},
+};
+bool Knob::allowed(int v) const {
+    if (field == &Tuning::lc_max_stride) return v == 12 || v == 16 || v == 18;
+    if (field == &Tuning::block_stage) return v == 0 || v == 256 || v == 512 || v == 1024;
+    return true;
+}
+}  // namespace
+
+int tuning_set(Tuning& t, const std::string& key, int value, bool* compiler) {
+    for (const Knob& k : kKnobs) {
+        if (key != k.key) continue;
+        if (value < k.lo || value > k.hi || !k.allowed(value)) return -1;
+        t.*(k.field) = (uint32_t)value;
+        if (compiler) *compiler = k.compiler;
+        return 0;
+    }
+    return -1;
+}
+
+int tuning_get(const Tuning& t, const std::string& key, int* value) {
+    for (const Knob& k : kKnobs) {
+        if (key != k.key) continue;
+        if (value) *value = (int)(t.*(k.field));
+        return 0;
+    }
+    return -1;
+}
 
 // ---- compile one vpp_acl rule (aclengine_mock.go:510-649) --------------------------------
 // Every outcome of evalACL for a rule is expressed as (src predicate, dst predicate,
@@ -84,6 +140,8 @@ DevRule compile_acl_rule(const AclRule& r) {
 
 // ---- Engine ------------------------------------------------------------------------------
 Engine::~Engine() {
+    if (comm) dev_comm_destroy(comm);
+    if (comm_check) dev_release(comm_check);
     if (cur) dev_free(cur);
     if (counters) dev_release(counters);
 }
@@ -160,7 +218,7 @@ int Engine::sync() {
         last_error = "upload: " + err;
         return PG_EIO;
     }
-    if (cur) dev_free(cur);  // dev_upload synchronises before returning: old set is idle
+    if (cur) dev_free(cur);  // waits for the launches that read the old set
     cur = nb;
     size_t slots = dev_view(cur).n_slots;
     if (slots != counter_slots) {
@@ -174,7 +232,7 @@ int Engine::sync() {
         counter_slots = slots;
     }
     // slot meanings change with the tables: counters restart from zero
-    if (dev_memset(counters, 0, slots * 8, nullptr, &err) != 0 || dev_sync(&err) != 0) {
+    if (dev_memset(counters, 0, slots * 8, nullptr, &err) != 0 || dev_stream_sync(nullptr, &err) != 0) {
         last_error = err;
         return PG_EIO;
     }
@@ -212,11 +270,12 @@ void Engine::compile() {
         std::vector<uint32_t> blob;
         hdr.dflt = (kActDeny << 30) | (NR + (uint32_t)t);
         bool ok = build_fast_table(h.rules.data() + hdr.rule_base, hdr.n_rules, hdr.rule_base, NR + (uint32_t)t, blob,
-                                   1ull << 22, &an[t]);
-        if (ok && (blob.size() > kStageBlobWords || (g_lc_lds && blob.size() >= g_lc_lds))) {  // fewer dependent loads in dense subtrees
+                                   1ull << 22, tune, &an[t]);
+        // fewer dependent loads in dense subtrees
+        if (ok && (blob.size() > kStageBlobWords || (tune.lc_lds && blob.size() >= tune.lc_lds))) {
             std::vector<uint32_t> lc;
             if (build_fast_table(h.rules.data() + hdr.rule_base, hdr.n_rules, hdr.rule_base, NR + (uint32_t)t, lc,
-                                 1ull << 22, nullptr, true) &&
+                                 1ull << 22, tune, nullptr, true) &&
                 (blob.size() > kStageBlobWords || lc.size() <= kStageBlobWords))
                 blob.swap(lc);
         }
@@ -237,6 +296,14 @@ void Engine::compile() {
     for (uint32_t t = 0; t < T; t++) slot_table.push_back((int32_t)t), slot_rule.push_back(-1);
     slot_table.push_back(-1), slot_rule.push_back(-1);  // no ACL
     slot_table.push_back(-1), slot_rule.push_back(-2);  // unresolved interface
+    layout_hash = 1469598103934665603ull;
+    auto fnv = [&](const void* p, size_t n) {
+        for (size_t i = 0; i < n; i++) layout_hash = (layout_hash ^ ((const uint8_t*)p)[i]) * 1099511628211ull;
+    };
+    for (uint32_t t = 0; t < T; t++) {
+        fnv(table_names[t].data(), table_names[t].size() + 1);
+        fnv(&h.tabs[t].n_rules, 4);
+    }
 
     // interfaces
     iface_index.clear();
@@ -289,7 +356,7 @@ void Engine::compile() {
     // node classifier for the PERPOD / CONN modes (same end points as the iphash)
     std::vector<NodePod> np;
     for (auto& e : ipmap) np.push_back(NodePod{e.ip, e.ifc, e.tin, e.tout});
-    build_node(h, an, np, NodePod{0, h.node_if, h.node_in, h.node_out});
+    build_node(h, an, np, NodePod{0, h.node_if, h.node_in, h.node_out}, tune);
     for (TableAnalysis* a : an) free_analysis(a);
     compiled = true;
 }

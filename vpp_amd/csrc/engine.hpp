@@ -22,6 +22,7 @@ DevRule compile_acl_rule(const AclRule& r);
 
 struct Engine {
     int device = 0;
+    Tuning tune = default_tuning();  // this context's knobs (pg_ctx_set_tuning)
     std::string last_error;
     NodeIfaces ifaces;
     std::map<PodID, PodReg> pods;
@@ -43,6 +44,17 @@ struct Engine {
     std::vector<int32_t> slot_table, slot_rule;
     unsigned long long* counters = nullptr;
     size_t counter_slots = 0;
+    uint64_t layout_hash = 0;  // FNV-64a over (table name, rule count) in slot order
+
+    // RCCL: one communicator per context (multi-process: pg_comm_init_rank; one process over
+    // several GPUs: pg_comm_init_all). Before every counter all-reduce the ranks compare
+    // (counter slots, layout hash) with a max all-reduce of this 4 x u64 device scratch.
+    void* comm = nullptr;
+    int comm_rank = -1, comm_nranks = 0;
+    unsigned long long* comm_check = nullptr;
+    // host copy of the counters as last all-reduced / read (pg_counters_snapshot: the
+    // statscollector gauge reads it without touching the GPU)
+    std::vector<uint64_t> snapshot;
 
     ~Engine();
     std::string apply_txn(bool resync, const AclOps& ops);

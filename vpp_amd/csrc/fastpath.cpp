@@ -64,18 +64,19 @@ struct VecHash {
 // and stride (blobwalk.hpp trie_child/trie_stride); children take 8-bit strides, or with
 // `lc` (level compression, for tries read from HBM) 18 / 16 / 12 bits when their span holds
 // at least 8192 / 2048 / 256 interval boundaries: about the memory of the 8-bit levels they
-// replace, one or two dependent loads fewer. 18-bit strides only when g_lc_max_stride allows
+// replace, one or two dependent loads fewer. 18-bit strides only when Tuning::lc_max_stride allows
 // (off by default: a 1 MiB child per 2^18 span made config 4's blob 13.8 MB, over the 4 MB
 // L2 of an XCD; at 16 it is 6.2 MB and 4 % faster).
 constexpr uint32_t kTrieFail = 0xFFFFFFFFu;
-uint32_t g_lc_dense12 = 16;  // boundaries in a child's span that earn it a 12-bit stride
-uint32_t g_lc_max_stride = 16;  // widest stride level compression may pick (A/B on MI355X, config 4: 16 = +4 % over 18, 12 = -3 %)
+// Tuning::lc_dense12: boundaries in a child's span that earn it a 12-bit stride;
+// Tuning::lc_max_stride: widest stride level compression may pick (A/B on MI355X, config 4:
+// 16 = +4 % over 18, 12 = -3 %)
 constexpr uint32_t kLcRootBits = 14;  // HBM-resident blobs: the root alone is staged in LDS (64 KiB)
 // `node`: the node image's encoding (blobwalk.hpp node_child): a non-leaf entry holds the
 // child's BYTE offset << 10 | stride << 5 | the address shift of the child level, so a step is
 // one bit-field extract and one shifted add; children must lie below 2 MiB.
 uint32_t build_trie(std::vector<uint32_t>& blob, const std::vector<uint64_t>& bnd, const std::vector<uint32_t>& cls,
-                    uint32_t W, uint32_t s1, bool lc = false, bool node = false) {
+                    uint32_t W, uint32_t s1, const Tuning& tu, bool lc = false, bool node = false) {
     // interval index containing address a
     auto find = [&](uint64_t a) { return (size_t)(std::upper_bound(bnd.begin(), bnd.end(), a) - bnd.begin()) - 1; };
     struct Job {
@@ -107,9 +108,9 @@ uint32_t build_trie(std::vector<uint32_t>& blob, const std::vector<uint64_t>& bn
             uint32_t st = std::min<uint32_t>(8, j.shift);
             if (lc && j.shift >= 12) {
                 const size_t inside = (size_t)(std::lower_bound(bnd.begin(), bnd.end(), a + span) - bnd.begin()) - k - 1;
-                if (g_lc_max_stride >= 18 && j.shift >= 18 && inside >= 8192) st = 18;
-                else if (g_lc_max_stride >= 16 && j.shift >= 16 && inside >= 2048) st = 16;
-                else if (inside >= g_lc_dense12) st = 12;
+                if (tu.lc_max_stride >= 18 && j.shift >= 18 && inside >= 8192) st = 18;
+                else if (tu.lc_max_stride >= 16 && j.shift >= 16 && inside >= 2048) st = 16;
+                else if (inside >= tu.lc_dense12) st = 12;
             }
             uint32_t child = (uint32_t)blob.size();
             if ((uint64_t)child + (1ull << st) > (node ? kNodeChildMaxWords : kTrieChildMask)) return kTrieFail;
@@ -121,27 +122,20 @@ uint32_t build_trie(std::vector<uint32_t>& blob, const std::vector<uint64_t>& bn
     return root;
 }
 
-uint32_t g_root_bits_max = 16;
-
 // root stride: enough root entries (~4 per interval boundary) that most lookups end at the
-// root or one level below, capped (a 2^16-entry root is 256 KiB)
-uint32_t pick_stride(size_t nb, uint32_t W) {
+// root or one level below, capped by Tuning::root_bits_max (a 2^16-entry root is 256 KiB)
+uint32_t pick_stride(size_t nb, uint32_t W, const Tuning& tu) {
     uint32_t s = 4;
-    while (s < g_root_bits_max && s < W && (1ull << s) < 4 * (uint64_t)nb) s += 4;
+    while (s < tu.root_bits_max && s < W && (1ull << s) < 4 * (uint64_t)nb) s += 4;
     return std::min(s, W);
 }
 
 bool unconditional(const DevRule& r) { return r.dmask == 0 && r.klo == 0 && r.khi == kKeyMax; }
 bool live(const DevRule& r) { return r.klo <= r.khi; }  // can match a TCP/UDP/OTHER packet
 
-uint32_t g_node_enable = 1;
-uint32_t g_lc_node = 0;  // level-compressed node tries (LDS image)
-uint32_t g_pair_enable = 1;  // PAIR mode for tables CROSS cannot take (else CAND); 2 = always
 constexpr uint32_t kPairMaxRules = 1u << 16;
 constexpr uint64_t kPairBudget = 1ull << 22;  // entries of each PAIR phase table (16 MiB)
 constexpr size_t kPairListMin = 16;  // CROSS dst lists longer than this: PAIR instead
-uint32_t g_node_common = 1;               // common-row section of the node image
-uint32_t g_node_root_bits = 12;           // node IPv4 trie root: 2^12 words = 16 KiB
 constexpr uint64_t kNodeCrossBudget = 1ull << 25;  // node cross entries (128 MiB)
 
 }  // namespace
@@ -162,19 +156,9 @@ struct TableAnalysis {
 
 void free_analysis(TableAnalysis* an) { delete an; }
 
-void set_root_bits_max(uint32_t bits) { g_root_bits_max = std::max<uint32_t>(4, std::min<uint32_t>(16, bits)); }
-void set_lc_node(uint32_t on) { g_lc_node = on; }
-void set_pair_enable(uint32_t on) { g_pair_enable = on; }
-void set_lc_dense12(uint32_t n) { g_lc_dense12 = n; }
-void set_lc_max_stride(uint32_t s) { g_lc_max_stride = s; }
-void set_node_common(uint32_t on) { g_node_common = on; }
-void set_node_tuning(uint32_t enable, uint32_t root_bits) {
-    g_node_enable = enable;
-    g_node_root_bits = std::max<uint32_t>(4, std::min<uint32_t>(16, root_bits));
-}
-
 bool build_fast_table(const DevRule* rules, uint32_t n, uint32_t rule_base, uint32_t default_slot,
-                      std::vector<uint32_t>& blob, uint64_t cross_budget, TableAnalysis** an, bool lc) {
+                      std::vector<uint32_t>& blob, uint64_t cross_budget, const Tuning& tu, TableAnalysis** an,
+                      bool lc) {
     if (an) *an = nullptr;
     blob.assign(16, 0);
     const uint32_t dflt = (kActDeny << 30) | default_slot;
@@ -250,7 +234,7 @@ bool build_fast_table(const DevRule* rules, uint32_t n, uint32_t rule_base, uint
     blob[10] = nsc;
 
     // ---- key classes and the cross product, if it fits ---------------------------------------
-    bool cross = n <= 16384 && g_pair_enable != 2;  // pair = 2: PAIR wherever it fits (tests)
+    bool cross = n <= 16384 && tu.pair != 2;  // pair = 2: PAIR wherever it fits (tests)
     std::vector<uint64_t> kb{0};
     std::vector<uint32_t> kseg_cls;
     std::vector<std::vector<uint32_t>> key_sets;  // sorted rule indices covering the segment
@@ -417,12 +401,12 @@ bool build_fast_table(const DevRule* rules, uint32_t n, uint32_t rule_base, uint
                                 break;
                             }
                     }
-                const uint32_t s1 = std::min<uint32_t>(pick_stride(sb.size(), 32), lc ? kLcRootBits : 32u);
-                if (build_trie(blob, sb, sint_cls, 32, s1, lc) != kSrcRoot) return false;
-                const uint32_t k1 = pick_stride(kb.size(), 18);
-                const uint32_t kroot = build_trie(blob, kb, kseg_cls, 18, k1, lc);
-                const uint32_t d1 = pick_stride(db.size(), 32);
-                const uint32_t droot = kroot == kTrieFail ? kTrieFail : build_trie(blob, db, dint_cls, 32, d1, lc);
+                const uint32_t s1 = std::min<uint32_t>(pick_stride(sb.size(), 32, tu), lc ? kLcRootBits : 32u);
+                if (build_trie(blob, sb, sint_cls, 32, s1, tu, lc) != kSrcRoot) return false;
+                const uint32_t k1 = pick_stride(kb.size(), 18, tu);
+                const uint32_t kroot = build_trie(blob, kb, kseg_cls, 18, k1, tu, lc);
+                const uint32_t d1 = pick_stride(db.size(), 32, tu);
+                const uint32_t droot = kroot == kTrieFail ? kTrieFail : build_trie(blob, db, dint_cls, 32, d1, tu, lc);
                 if (droot == kTrieFail) return false;
                 while (blob.size() % 4) blob.push_back(0);
                 const size_t poff = blob.size();
@@ -450,18 +434,18 @@ bool build_fast_table(const DevRule* rules, uint32_t n, uint32_t rule_base, uint
     };
 
     // long dst lists: PAIR's two lookups beat a record scan (unless it does not fit)
-    if (cross && lists && max_list > kPairListMin && g_pair_enable && n <= kPairMaxRules) {
+    if (cross && lists && max_list > kPairListMin && tu.pair && n <= kPairMaxRules) {
         if (try_pair()) return true;
         blob_header_only();
     }
     if (cross) {
         const uint32_t nkc = (uint32_t)key_sets.size();
-        const uint32_t s1 = std::min<uint32_t>(pick_stride(sb.size(), 32), lc ? kLcRootBits : 32u);
-        if (build_trie(blob, sb, sint_cls, 32, s1, lc) != kSrcRoot) return false;
+        const uint32_t s1 = std::min<uint32_t>(pick_stride(sb.size(), 32, tu), lc ? kLcRootBits : 32u);
+        if (build_trie(blob, sb, sint_cls, 32, s1, tu, lc) != kSrcRoot) return false;
         blob[2] = kSrcRoot;
         blob[3] = s1;
-        const uint32_t k1 = pick_stride(kb.size(), 18);
-        blob[4] = build_trie(blob, kb, kseg_cls, 18, k1, lc);
+        const uint32_t k1 = pick_stride(kb.size(), 18, tu);
+        blob[4] = build_trie(blob, kb, kseg_cls, 18, k1, tu, lc);
         if (blob[4] == kTrieFail) return false;
         blob[5] = k1;
         blob[7] = nkc;
@@ -506,7 +490,7 @@ bool build_fast_table(const DevRule* rules, uint32_t n, uint32_t rule_base, uint
         return true;
     }
 
-    if (!cross && g_pair_enable && n <= kPairMaxRules && try_pair()) return true;
+    if (!cross && tu.pair && n <= kPairMaxRules && try_pair()) return true;
     blob_header_only();
 
     // ---- candidate mode: src trie leaves point at the class's record list -------------------
@@ -519,8 +503,8 @@ bool build_fast_table(const DevRule* rules, uint32_t n, uint32_t rule_base, uint
     if (nrec >= (1ull << 29)) return false;
     std::vector<uint32_t> leaf(sb.size());
     for (size_t k = 0; k < sb.size(); k++) leaf[k] = first_rec[sint_cls[k]];
-    const uint32_t s1 = std::min<uint32_t>(pick_stride(sb.size(), 32), lc ? kLcRootBits : 32u);
-    if (build_trie(blob, sb, leaf, 32, s1, lc) != kSrcRoot) return false;
+    const uint32_t s1 = std::min<uint32_t>(pick_stride(sb.size(), 32, tu), lc ? kLcRootBits : 32u);
+    if (build_trie(blob, sb, leaf, 32, s1, tu, lc) != kSrcRoot) return false;
     blob[0] = kFlagCand;
     blob[2] = kSrcRoot;
     blob[3] = s1;
@@ -555,12 +539,13 @@ bool build_fast_table(const DevRule* rules, uint32_t n, uint32_t rule_base, uint
 // the cross table. Appended after the base image; the kernels stage and use it when the LDS
 // budget allows (device.hip). Skipped when the bitmap would exceed kCommonMapMaxBits.
 constexpr uint64_t kCommonMapMaxBits = 1ull << 20;  // 128 KiB
-void build_common_rows(HostTableSet& h, const std::vector<uint32_t>& cov, const std::vector<TableAnalysis*>& an) {
+void build_common_rows(HostTableSet& h, const std::vector<uint32_t>& cov, const std::vector<TableAnalysis*>& an,
+                       const Tuning& tu) {
     std::vector<uint32_t>& img = h.node_img;
     DevNode& N = h.node;
     const uint32_t T = (uint32_t)h.tabs.size(), G = N.n_ipc;
     const uint64_t bits = (uint64_t)T * G;
-    if (!g_node_common || bits > kCommonMapMaxBits) return;
+    if (!tu.node_common || bits > kCommonMapMaxBits) return;
     const std::vector<uint32_t>& X = h.node_cross;
     std::vector<uint32_t> sec, map((size_t)((bits + 31) / 32), 0);
     std::vector<uint32_t> crow(T, 0);
@@ -599,12 +584,12 @@ void build_common_rows(HostTableSet& h, const std::vector<uint32_t>& cov, const 
 }
 
 bool build_node(HostTableSet& h, const std::vector<TableAnalysis*>& an, const std::vector<NodePod>& pods,
-                const NodePod& node_end) {
+                const NodePod& node_end, const Tuning& tu) {
     h.node_img.clear();
     h.node_cross.clear();
     h.node = DevNode{};
     const uint32_t T = (uint32_t)h.tabs.size();
-    if (!g_node_enable || T == 0 || T >= 0xFFFFu) return false;
+    if (!tu.node_build || T == 0 || T >= 0xFFFFu) return false;
     std::vector<uint32_t> cov;
     for (uint32_t t = 0; t < T; t++)
         if (an[t] && an[t]->nkc <= 0xFFFFu) cov.push_back(t);
@@ -681,10 +666,10 @@ bool build_node(HostTableSet& h, const std::vector<TableAnalysis*>& an, const st
     // image: tries, ipinfo, tabinfo, kmap
     std::vector<uint32_t>& img = h.node_img;
     DevNode& N = h.node;
-    N.ip_s1 = std::min(pick_stride(gb.size(), 32), g_node_root_bits);
-    if (build_trie(img, gb, gcls, 32, N.ip_s1, g_lc_node != 0, true) != 0) return false;
-    N.key_k1 = std::min(pick_stride(kb.size(), 18), g_node_root_bits);
-    N.key_root = build_trie(img, kb, kcls, 18, N.key_k1, false, true);
+    N.ip_s1 = std::min(pick_stride(gb.size(), 32, tu), tu.node_root_bits);
+    if (build_trie(img, gb, gcls, 32, N.ip_s1, tu, tu.lc_node != 0, true) != 0) return false;
+    N.key_k1 = std::min(pick_stride(kb.size(), 18, tu), tu.node_root_bits);
+    N.key_root = build_trie(img, kb, kcls, 18, N.key_k1, tu, false, true);
     if (N.key_root == kTrieFail) return false;
     while (img.size() % 2) img.push_back(0);
     N.ipinfo = (uint32_t)img.size();
@@ -748,7 +733,7 @@ bool build_node(HostTableSet& h, const std::vector<TableAnalysis*>& an, const st
             }
         }
     }
-    build_common_rows(h, cov, an);
+    build_common_rows(h, cov, an, tu);
     X.resize(rec0, 0);
     X.insert(X.end(), recs.begin(), recs.end());
     if (X.empty()) X.resize(4, 0);

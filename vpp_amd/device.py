@@ -115,6 +115,52 @@ def reset_counters(engine, stream=None):
     engine._ck(lib.pg_reset_counters(engine.h, _stream_ptr(stream)))
 
 
+def counters_snapshot(engine):
+    """host snapshot of the last read / all-reduce (pg_counters_snapshot: no GPU access)"""
+    n = engine._ck(lib.pg_counters_snapshot(engine.h, None, 0))
+    buf = (C.c_uint64 * max(1, n))()
+    engine._ck(lib.pg_counters_snapshot(engine.h, buf, n))
+    return np.frombuffer(buf, dtype=np.uint64)[:n].copy()
+
+
+# ---- RCCL counter all-reduce through the C ABI (include/policygpu.h pg_comm_*) -------------
+def comm_unique_id():
+    buf = C.create_string_buffer(128)
+    rc = lib.pg_comm_unique_id(buf)
+    if rc < 0:
+        raise RuntimeError("pg_comm_unique_id failed (%d)" % rc)
+    return buf.raw
+
+
+def comm_init_rank(engine, nranks, uid, rank):
+    engine._ck(lib.pg_comm_init_rank(engine.h, nranks, C.create_string_buffer(uid, 128), rank))
+
+
+def comm_init_all(engines):
+    arr = (C.c_void_p * len(engines))(*[e.h for e in engines])
+    rc = lib.pg_comm_init_all(arr, len(engines))
+    if rc < 0:
+        engines[0]._ck(rc)
+
+
+def allreduce_counters(engine, stream=None):
+    """sum this rank's device counters over the communicator (in place) -> the summed counters"""
+    engine._ck(lib.pg_allreduce_counters(engine.h, _stream_ptr(stream)))
+    return counters_snapshot(engine)
+
+
+def allreduce_counters_all(engines):
+    arr = (C.c_void_p * len(engines))(*[e.h for e in engines])
+    rc = lib.pg_allreduce_counters_all(arr, len(engines))
+    if rc < 0:
+        for e in engines:
+            msg = lib.pg_last_error(e.h).decode()
+            if msg:
+                raise RuntimeError("%s (code %d)" % (msg, rc))
+        raise RuntimeError("pg_allreduce_counters_all failed (%d)" % rc)
+    return [counters_snapshot(e) for e in engines]
+
+
 def unpack(out_u32):
     w = out_u32.astype(np.uint32)
     return (w >> 30).astype(np.int64), (w & 0x3FFFFFFF).astype(np.int64)

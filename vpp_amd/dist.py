@@ -46,6 +46,15 @@ def allreduce_counters(counters, group=None):
     return counters
 
 
+def sum_over_ranks(value, device):
+    """Sum of an integer over all ranks (tuples of the whole job)."""
+    if not (dist.is_initialized() and dist.get_world_size() > 1):
+        return int(value)
+    t = torch.tensor([int(value)], dtype=torch.int64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return int(t.item())
+
+
 def max_over_ranks(value, device):
     """Max of a float over all ranks (the bench's wall time)."""
     if not (dist.is_initialized() and dist.get_world_size() > 1):

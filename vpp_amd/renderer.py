@@ -140,6 +140,35 @@ class Engine:
             raise PolicyError(rc, lib.pg_last_error(self.h).decode())
         return rc
 
+    # tuning knobs of this context (pg_ctx_set_tuning; include/policygpu.h lists the keys)
+    def set_tuning(self, key, value):
+        self._ck(lib.pg_ctx_set_tuning(self.h, _b(key), int(value)))
+
+    def get_tuning(self, key):
+        v = C.c_int()
+        self._ck(lib.pg_ctx_get_tuning(self.h, _b(key), C.byref(v)))
+        return v.value
+
+    def tuning(self, **kw):
+        """context manager: the given knobs set for the block, restored afterwards"""
+        import contextlib
+
+        @contextlib.contextmanager
+        def cm():
+            old = {k: self.get_tuning(k) for k in kw}
+            try:
+                for k, v in kw.items():
+                    self.set_tuning(k, v)
+                yield self
+            finally:
+                for k, v in old.items():
+                    self.set_tuning(k, v)
+        return cm()
+
+    @property
+    def device(self):
+        return self._ck(lib.pg_ctx_device(self.h))
+
     # ipv4net / contivconf setters
     def SetPodIfName(self, pod, if_name):
         ns, name = _pod(pod)
