@@ -30,7 +30,6 @@ from vpp_amd import workloads as W  # noqa: E402
 
 METRIC = "classified 5-tuples/sec (Mpps) at 1/2/4/8 GPUs vs rule count; % of HBM peak"
 HBM_PEAK_GBS = 8000.0           # MI355X HBM3E spec (MI355X_MICROARCH.md)
-BYTES_PER_TUPLE = {0: 15, 1: 15, 2: 17}   # 11 B in + 4 B out (+2 B sport in CONN)
 MODE_NAME = {0: "single", 1: "perpod", 2: "conn"}
 
 
@@ -146,7 +145,8 @@ def main():
     if world > 1:
         allreduce = counter_allreduce(e, w, b, out, rank, world)
 
-    achieved = n * BYTES_PER_TUPLE[w.mode] / (kern_ms * 1e-3) / 1e9
+    bpt, fields = bytes_per_tuple(w)
+    achieved = n * bpt / (kern_ms * 1e-3) / 1e9
     traffic, traffic_src = pmc_traffic(a.config, n, a.counters and not w.counters)
     line = {
         "metric": METRIC, "value": round(mpps, 1), "unit": "Mpps", "n_gpus": world, "steps": a.steps,
@@ -158,8 +158,8 @@ def main():
                    "counters": bool(use_counters), "classifier": classifier(w, a.per_table)},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                     "bytes_per_tuple": BYTES_PER_TUPLE[w.mode], "kernel_ms": round(kern_ms, 4),
-                     "algorithmic_bytes_per_launch": n * BYTES_PER_TUPLE[w.mode], "traffic_source": traffic_src},
+                     "bytes_per_tuple": bpt, "fields": fields, "kernel_ms": round(kern_ms, 4),
+                     "algorithmic_bytes_per_launch": n * bpt, "traffic_source": traffic_src},
     }
     if allreduce is not None:
         line.update(allreduce)
@@ -244,6 +244,19 @@ def dry_run(a, rank, world):
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def bytes_per_tuple(w):
+    """Algorithmic bytes per tuple: the tuple fields the classification reads
+    plus the 4-B verdict. SINGLE / PERPOD read src 4 + dst 4 + dport 2 + proto 1 = 11 B (15 B
+    with the verdict), CONN also sport (17 B) -- except SINGLE over a table no rule of which
+    tests dst (compiled to the FD form): its verdict cannot depend on dst and the kernel does
+    not read that stream, so 7 B in + 4 B out = 11 B."""
+    if w.mode == 0 and w.engine.table_stats(w.table_id)["structure"] == "fd":
+        return 11, "src 4 + dport 2 + proto 1 in, verdict 4 out (no rule tests dst: dst not read)"
+    if w.mode == 2:
+        return 17, "src 4 + dst 4 + sport 2 + dport 2 + proto 1 in, verdict 4 out"
+    return 15, "src 4 + dst 4 + dport 2 + proto 1 in, verdict 4 out"
 
 
 def classifier(w, per_table):

@@ -163,3 +163,42 @@ def test_candidate_mode_multi_record_lists():
               [(192 << 24) | (168 << 16) | (k << 8) for k in range(5)]
     tup = fz.rand_tuples(np.random.default_rng(24), 30000, anchors)
     check(e, "big", rules, tup)
+
+
+@pytest.mark.parametrize("seed", range(10))
+def test_fd_tables_dst_free(seed):
+    """Tables where no rule tests dst (the renderer's pod tables, config 2) compile to the FD
+    form (fixed-depth walks, no dst stream; fastpath.cpp build_fd_blob) and classify like
+    evalACL -- ANY-protocol packets included -- and like the same tables compiled without it."""
+    rnd = random.Random(700 + seed)
+    rules = fz.rand_acl(rnd, rnd.choice([1, 5, 40, 300, 1000]), fz.ANCHORS, weird=(seed % 2 == 1),
+                        tail=rnd.choice([None, "deny", "permit"]))
+    for r in rules:
+        r["dst"] = ""
+    plain = [r for r in rules if not any(r.get(k) for k in ("macip", "icmp")) and r.get("ip_rule", True)
+             and r.get("ip", True) and not (r.get("tcp") and r.get("udp"))]
+    rules = plain or [{"action": 1, "src": "", "dst": ""}]
+    e = engine_with({"fd": rules})
+    st = e.table_stats(0)
+    tup = fz.rand_tuples(np.random.default_rng(seed), 30000, fz.ANCHORS, any_pct=0.05)
+    check(e, "fd", rules, tup)
+    got = e.debug_walk("fd", *[tup[k] for k in (0, 1, 3, 4)])
+    # the verdict does not depend on dst
+    tup2 = (tup[0], np.random.default_rng(seed + 1).integers(0, 1 << 32, len(tup[0]), dtype=np.uint64).astype(
+        np.uint32)) + tup[2:]
+    assert np.array_equal(e.debug_walk("fd", *[tup2[k] for k in (0, 1, 3, 4)]), got)
+    e0 = R.Engine(0)
+    e0.set_tuning("fd", 0)
+    e0.ApplyTxn(True, [("config/vpp/acls/v2/acl/fd", {"name": "fd", "rules": rules, "ingress": [],
+                                                       "egress": ["if-fd"]})])
+    assert e0.table_stats(0)["structure"] != "fd"
+    assert np.array_equal(e0.debug_walk("fd", *[tup[k] for k in (0, 1, 3, 4)]), got)
+    # not FD only when the FD form would not fit LDS (or the table is no cross product)
+    assert st["structure"] == "fd" or st["structure"] in ("cand", "pair", "linear") or st["blob_bytes"] > 48 << 10, st
+
+
+def test_config2_table_is_fd():
+    from vpp_amd import workloads as W
+    w = W.config2(0, n_tuples=1 << 10)
+    st = w.engine.table_stats(w.table_id)
+    assert st["structure"] == "fd" and st["blob_bytes"] <= 64 << 10 and st["key_classes"] == 21, st

@@ -20,6 +20,10 @@
 namespace pg {
 
 constexpr uint32_t kFlagCross = 1u, kFlagLists = 2u, kFlagCand = 4u, kFlagLinear = 8u, kFlagPair = 16u;
+// FD ("fixed depth", fastpath.cpp build_fd_blob): a CROSS table whose verdict does not
+// depend on the dst address, laid out so that every lookup is exactly D dependent reads per
+// field and one verdict read, with no per-lane branches (fd_walk below).
+constexpr uint32_t kFlagFD = 32u;
 constexpr uint32_t kPairHdr = 12u;  // PAIR blob header words: dst root, d1, pair table, n_dst_classes
 constexpr uint32_t kLeaf = 0x80000000u;
 // non-leaf trie entry: child block offset (words) | child stride << kTrieStrideShift
@@ -206,9 +210,38 @@ PG_HD void blob_walk(const L (&ld)[Q], const BlobTab (&tb)[Q], const bool (&on)[
     blob_walk<PRED>(ld, ld, tb, on, src, dst, key, w);
 }
 
+// FD blob walk (layout: fastpath.cpp build_fd_blob). Tries in the node encoding (non-leaf
+// entry = child byte offset << 10 | stride << 5 | shift); a leaf is a pointer to a word that
+// points to itself (stride 0), so a finished lookup re-reads that word and every lookup takes
+// the same D reads: src -> the self word heading its src class's verdict row, key -> the self
+// word of its key class. Verdict = the word at (src self) + (key self) + bias, i.e. row[1 +
+// key class]. fsk: s1 << 8 | k1 << 16; kroot: key trie root (words); depth: reads per field;
+// bias: 4 - 4 * (first key self word). ld must provide at_byte.
+template <class L, int Q>
+PG_HD void fd_walk(const L& ld, uint32_t fsk, uint32_t kroot, uint32_t depth, uint32_t bias, const uint32_t (&src)[Q],
+                   const uint32_t (&key)[Q], uint32_t (&w)[Q]) {
+    const uint32_t ss = 32u - ((fsk >> 8) & 0xFFu), sk = 18u - ((fsk >> 16) & 0xFFu);
+    uint32_t es[Q], ek[Q];
+    PG_UNROLL
+    for (int j = 0; j < Q; j++) {
+        es[j] = ld.at_byte(4u * kSrcRoot + ((src[j] >> ss) << 2));
+        ek[j] = ld.at_byte(4u * kroot + ((key[j] >> sk) << 2));
+    }
+    for (uint32_t l = 1; l < depth; l++) {
+        PG_UNROLL
+        for (int j = 0; j < Q; j++) {
+            es[j] = ld.at_byte(node_child_byte(es[j], src[j]));
+            ek[j] = ld.at_byte(node_child_byte(ek[j], key[j]));
+        }
+    }
+    PG_UNROLL
+    for (int j = 0; j < Q; j++) w[j] = ld.at_byte((es[j] >> 10) + (ek[j] >> 10) + bias);
+}
+
 struct HostLoader {
     const uint32_t* b;
     uint32_t u32(uint32_t i) const { return b[i]; }
+    uint32_t at_byte(uint32_t off) const { return b[off >> 2]; }
     W2 u2(uint32_t i) const { return W2{b[i], b[i + 1]}; }
     W4 u4(uint32_t i) const { return W4{b[i], b[i + 1], b[i + 2], b[i + 3]}; }
 };

@@ -454,7 +454,8 @@ int pg_table_stats(pg_ctx* ctx, int table_id, uint32_t* flags, uint32_t* blob_by
     if (flags) *flags = hd.fsk & 0xFFu;
     if (blob_bytes) *blob_bytes = words * 4;
     if (n_src_classes) *n_src_classes = words ? b[10] : 0;
-    if (n_key_classes) *n_key_classes = (words && (hd.fsk & (kFlagCross | kFlagPair))) ? b[7] : 0;
+    if (n_key_classes)
+        *n_key_classes = !words ? 0 : (hd.fsk & kFlagFD) ? b[8] : (hd.fsk & (kFlagCross | kFlagPair)) ? b[7] : 0;
     return PG_OK;
     GUARD_END(ctx)
 }
@@ -469,6 +470,17 @@ int pg_debug_walk_blob(pg_ctx* ctx, const char* acl_name, const uint32_t* src, c
     if (it == E.table_of_acl.end()) return fail(ctx, PG_ENOENT, "no such ACL");
     const DevTable& hd = E.host.tabs[it->second];
     const bool linear = (hd.fsk & kFlagLinear) != 0;
+    if (hd.fsk & kFlagFD) {  // the FD walk (one tuple at a time; ANY keys: linear, dst unused)
+        DevTableSet T{};
+        T.rules = E.host.rules.data();
+        for (uint64_t i = 0; i < n; i++) {
+            const uint32_t s1[1] = {src[i]}, dp1[1] = {dst_port[i]}, pr1[1] = {proto[i]};
+            uint32_t w1[1];
+            classify_fd_q<false, 1>(T, E.host.blobs.data() + hd.blob_off, hd, s1, dp1, pr1, Hist{nullptr, nullptr}, w1);
+            out[i] = w1[0];
+        }
+        return PG_OK;
+    }
     // the kernels' lockstep walk, 4 tuples at a time
     constexpr int Q = 4;
     HostLoader ld[Q];

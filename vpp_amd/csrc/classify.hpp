@@ -110,7 +110,7 @@ PG_HD void eval_q(const DevTableSet& T, const uint32_t* blobs, const DevTable (&
                   const uint32_t* rootb = nullptr) {
     DevLoader ld[Q], ld0[Q];
     BlobTab tb[Q];
-    bool on[Q];
+    bool on[Q], fd[Q], anyfd = false;
     // on[j] depends on the table only (uniform when every lane has the same table, as in
     // SINGLE mode); ANY-protocol keys (< 2^18, a valid trie address) are walked too and their
     // result replaced by the linear scan below
@@ -119,12 +119,24 @@ PG_HD void eval_q(const DevTableSet& T, const uint32_t* blobs, const DevTable (&
         ld[j] = DevLoader{blobs + tab[j].blob_off};
         ld0[j] = rootb ? DevLoader{rootb} : ld[j];
         tb[j] = BlobTab{tab[j].fsk, tab[j].dflt, tab[j].kroot, tab[j].xoff, tab[j].nkc};
-        on[j] = act[j] && !(tab[j].fsk & kFlagLinear);
+        fd[j] = act[j] && (tab[j].fsk & kFlagFD);
+        on[j] = act[j] && !fd[j] && !(tab[j].fsk & kFlagLinear);
+        anyfd |= fd[j];
     }
     blob_walk<PRED>(ld, ld0, tb, on, src, dst, key, w);
+    if (anyfd) {  // FD tables, one lane at a time (their walk has no per-lane state to share)
+        PG_UNROLL
+        for (int j = 0; j < Q; j++) {
+            if (!fd[j]) continue;
+            const uint32_t s1[1] = {src[j]}, k1[1] = {key[j]};
+            uint32_t w1[1];
+            fd_walk(ld[j], tab[j].fsk, tab[j].kroot, tab[j].xoff, tab[j].nkc, s1, k1, w1);
+            w[j] = w1[0];
+        }
+    }
     PG_UNROLL
     for (int j = 0; j < Q; j++)
-        if (act[j] && (!on[j] || key[j] >= kWalkKeyLimit))
+        if (act[j] && ((!on[j] && !fd[j]) || key[j] >= kWalkKeyLimit))
             w[j] = eval_linear(T.rules, tab[j].rule_base, tab[j].n_rules, tab[j].dflt, src[j], dst[j], key[j]);
 }
 
@@ -203,6 +215,29 @@ struct Hist {
 #endif
     }
 };
+
+// SINGLE mode over an FD table (uniform: tab0), its blob at `blob` (the LDS copy in the kernels):
+// Q tuples per lane, fixed-depth walks in lockstep; ANY-protocol packets take the linear scan.
+// The dst address is not an input: no rule of an FD table tests it (engine.cpp compile).
+template <bool COUNT, int Q>
+PG_HD void classify_fd_q(const DevTableSet& T, const uint32_t* blob, const DevTable& tab0, const uint32_t (&s)[Q],
+                         const uint32_t (&dp)[Q], const uint32_t (&pr)[Q], const Hist& h, uint32_t (&out)[Q]) {
+    uint32_t key[Q];
+    bool any = false;
+    PG_UNROLL
+    for (int j = 0; j < Q; j++) key[j] = pkt_key(pr[j], dp[j]), any |= key[j] >= kWalkKeyLimit;
+    fd_walk(DevLoader{blob}, tab0.fsk, tab0.kroot, tab0.xoff, tab0.nkc, s, key, out);
+    if (any) {
+        PG_UNROLL
+        for (int j = 0; j < Q; j++)  // no rule of an FD table tests dst (engine.cpp): any dst will do
+            if (key[j] >= kWalkKeyLimit)
+                out[j] = eval_linear(T.rules, tab0.rule_base, tab0.n_rules, tab0.dflt, s[j], 0u, key[j]);
+    }
+    if (COUNT) {
+        PG_UNROLL
+        for (int j = 0; j < Q; j++) h.inc(out[j] & kSlotMask);
+    }
+}
 
 // ---- evaluators: evalACL of Q tuples on tables t[j], forward (src -> dst, SYN key) or
 // reverse (dst -> src, SYN-ACK key; testConnection's second half) ----------------------------

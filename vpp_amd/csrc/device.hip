@@ -321,7 +321,9 @@ __device__ __forceinline__ void stream_store(V v, V* p) {
 // STAGE (SINGLE mode): 1 = the table's blob (stage_words u32, multiple of 4) is copied into
 // LDS once per workgroup and every lookup of the grid-stride loop reads it from there; 2 = a
 // blob too large for LDS has its header and src-trie root (stage_words) copied, so the first
-// dependent load of every lookup hits LDS and the rest read HBM / L2.
+// dependent load of every lookup hits LDS and the rest read HBM / L2; 4 = an FD blob
+// (fastpath.cpp build_fd_blob) staged like 1 and walked by classify_fd_q: fixed-depth reads,
+// no per-lane branches, and no dst stream (no rule of an FD table tests dst).
 // NODE (PERPOD / CONN): the node classifier; STAGE then copies the node image into LDS.
 //
 // Stream pipelining (PG_PREFETCH): 1 = the next group's loads are issued at the top of each
@@ -356,6 +358,12 @@ __device__ __forceinline__ void stream_store(V v, V* p) {
 #endif
 #ifndef PG_QCONN_COUNT  // CONN with hit counters (A/B on MI355X, config 5: 2 = +9 % over 1, 4 = -6 %)
 #define PG_QCONN_COUNT 2
+#endif
+#ifndef PG_QSINGLE_FD  // SINGLE over an LDS-staged FD table (STAGE 4)
+#define PG_QSINGLE_FD 1
+#endif
+#ifndef PG_PREFETCH_FD  // STAGE 4: stream prefetch of the next group (see PG_PREFETCH)
+#define PG_PREFETCH_FD 0
 #endif
 #ifndef PG_TPL  // tuples per lane per loop iteration (4 or 8)
 #define PG_TPL 4
@@ -418,7 +426,7 @@ void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
         if (STAGE) {
             const uint4* g = reinterpret_cast<const uint4*>(T.blobs + tab0.blob_off);
             for (uint32_t i = threadIdx.x; i < stage_words / 4u; i += BS) reinterpret_cast<uint4*>(smem)[i] = g[i];
-            if (STAGE == 1) {
+            if (STAGE == 1 || STAGE == 4) {
                 blobs = smem;
                 tab0.blob_off = 0;
             }
@@ -443,11 +451,14 @@ void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
         Words<P / 2> dp, sp;
         Words<P / 4> pr;
     };
+    // STAGE 4 (SINGLE over an FD table): no rule tests dst, so the dst stream is not read
+    constexpr bool NEED_DST = !(MODE == 0 && STAGE == 4);
     auto load = [&](uint64_t q) {
         Group x;
         const uint64_t i0 = q * P;
         x.s = ld_words<P>(src + i0);
-        x.d = ld_words<P>(dst + i0);
+        if (NEED_DST) x.d = ld_words<P>(dst + i0);
+        else x.d = Words<P>{};
         x.dp = ld_words<P / 2>(reinterpret_cast<const uint32_t*>(dport + i0));
         x.pr = ld_words<P / 4>(reinterpret_cast<const uint32_t*>(proto + i0));
         if (MODE == 2) x.sp = ld_words<P / 2>(reinterpret_cast<const uint32_t*>(sport + i0));
@@ -456,7 +467,7 @@ void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
     };
     uint64_t q = first;
     Group cur;
-    constexpr int PF = PG_PREFETCH >= 0 ? PG_PREFETCH : (MODE == 0 ? 0 : 1);
+    constexpr int PF = STAGE == 4 ? PG_PREFETCH_FD : (PG_PREFETCH >= 0 ? PG_PREFETCH : (MODE == 0 ? 0 : 1));
     if (PF && q < nfull) cur = load(q);
     while (q < nfull) {
         const uint64_t qn = q + stride;
@@ -482,14 +493,18 @@ void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
         // per-mode chunk: the group's P tuples are classified QC at a time (less state per
         // lane, more waves per SIMD)
         constexpr int QC = MODE == 2 ? (COUNT ? PG_QCONN_COUNT : PG_QCONN)
-                                     : (MODE == 1 ? PG_QPOD : (STAGE == 1 ? PG_QSINGLE_LDS : PG_QSINGLE));
+                                     : (MODE == 1 ? PG_QPOD
+                                                  : (STAGE == 4 ? PG_QSINGLE_FD
+                                                                : (STAGE == 1 ? PG_QSINGLE_LDS : PG_QSINGLE)));
 #pragma unroll
         for (int c = 0; c < P; c += QC) {
             uint32_t cs[QC], cd[QC], csp[QC], cdp[QC], cpr[QC], co[QC];
 #pragma unroll
             for (int j = 0; j < QC; j++)
                 cs[j] = sv[c + j], cd[j] = dv[c + j], csp[j] = spv[c + j], cdp[j] = dpv[c + j], cpr[j] = prv[c + j];
-            if constexpr (NODE) {
+            if constexpr (MODE == 0 && STAGE == 4) {
+                classify_fd_q<COUNT, QC>(T, smem, tab0, cs, cdp, cpr, h, co);
+            } else if constexpr (NODE) {
                 if (c == 0)
                     classify_node_q<MODE, COUNT, QC, STAGE && PG_PRED, STAGE == 3>(T, T.node, img, cs, cd, csp, cdp, cpr, h, co, hook);
                 else
@@ -510,10 +525,11 @@ void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
     }
     // remainder (or everything when the pointers are not vector-aligned): one tuple per lane
     for (uint64_t i = nfull * P + first; i < n; i += stride) {
-        const uint32_t s1[1] = {src[i]}, d1[1] = {dst[i]}, sp1[1] = {MODE == 2 ? (uint32_t)sport[i] : 0u},
-                       dp1[1] = {dport[i]}, pr1[1] = {proto[i]};
+        const uint32_t s1[1] = {src[i]}, d1[1] = {NEED_DST ? dst[i] : 0u},
+                       sp1[1] = {MODE == 2 ? (uint32_t)sport[i] : 0u}, dp1[1] = {dport[i]}, pr1[1] = {proto[i]};
         uint32_t o[1];
-        if constexpr (NODE) classify_node_q<MODE, COUNT, 1, STAGE && PG_PRED, STAGE == 3>(T, T.node, img, s1, d1, sp1, dp1, pr1, h, o);
+        if constexpr (MODE == 0 && STAGE == 4) classify_fd_q<COUNT, 1>(T, smem, tab0, s1, dp1, pr1, h, o);
+        else if constexpr (NODE) classify_node_q<MODE, COUNT, 1, STAGE && PG_PRED, STAGE == 3>(T, T.node, img, s1, d1, sp1, dp1, pr1, h, o);
         else classify_q<MODE, COUNT, 1, STAGE == 1 && PG_PRED>(T, blobs, tab0, s1, d1, sp1, dp1, pr1, h, o, rootb);
         out[i] = o[0];
     }
@@ -731,7 +747,10 @@ static void launch_classify(const DevTableSet& T, const Tuning& tu, int t, const
         const DevTable& hd = T.host_tabs[t];
         const uint32_t words = T.host_blob_words[t];
         const uint32_t root_words = (kSrcRoot + (1u << ((hd.fsk >> 8) & 0xFFu)) + 3u) & ~3u;
-        if (!(hd.fsk & kFlagLinear) && words && words <= tu.stage_max_words)
+        if ((hd.fsk & kFlagFD) && words <= tu.stage_max_words)  // FD blob in LDS, no dst stream
+            launch_one<MODE, COUNT, VEC, 4, false>(T, tu, t, src, dst, sport, dport, proto, n, out, counters, st, hist,
+                                                   words, items);
+        else if (!(hd.fsk & kFlagLinear) && words && words <= tu.stage_max_words)
             launch_one<MODE, COUNT, VEC, 1, false>(T, tu, t, src, dst, sport, dport, proto, n, out, counters, st, hist,
                                                    words, items);
         else if (!(hd.fsk & kFlagLinear) && words && root_words <= tu.stage_root_max_words)

@@ -119,6 +119,7 @@ struct Tuning {
     uint32_t node_root_bits = 12;  // its IPv4 / key trie root stride cap (4..16)
     uint32_t lc_node = 0;          // level-compressed node IPv4 trie
     uint32_t node_common = 1;      // common-row section of node images
+    uint32_t fd = 1;               // FD form of dst-independent CROSS tables that fit LDS
     // launches
     uint32_t blocks_per_cu = 0;    // cap on resident workgroups per CU (0 = occupancy)
     uint32_t stage_max_words = kStageBlobWords;  // table blobs staged whole in LDS
@@ -142,6 +143,10 @@ bool build_fast_table(const DevRule* rules, uint32_t n, uint32_t rule_base, uint
                       std::vector<uint32_t>& blob, uint64_t cross_budget, const Tuning& tu,
                       TableAnalysis** an = nullptr, bool lc = false);
 void free_analysis(TableAnalysis* an);
+// fastpath.cpp: the FD (fixed-depth, dst-independent) form of a CROSS table without dst lists,
+// when it fits max_words (false otherwise; blobwalk.hpp fd_walk)
+bool build_fd_blob(const TableAnalysis& an, uint32_t dflt, const Tuning& tu, std::vector<uint32_t>& blob,
+                   uint32_t max_words);
 // fastpath.cpp: the node classifier over the tables with an analysis (null = not covered).
 // pods: {IPv4, interface, inbound table, outbound table} of local pods; node_end: the same for
 // every other address. false = over budget (h.node_img left empty).

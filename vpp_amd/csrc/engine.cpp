@@ -34,6 +34,7 @@ const Knob kKnobs[] = {
     {"node_root_bits", &Tuning::node_root_bits, 4, 16, true},
     {"lc_node", &Tuning::lc_node, 0, 1, true},
     {"node_common", &Tuning::node_common, 0, 1, true},
+    {"fd", &Tuning::fd, 0, 1, true},
     {"blocks_per_cu", &Tuning::blocks_per_cu, 0, 64, false},
     {"stage_max_words", &Tuning::stage_max_words, 0, 36864, false},
     {"node_stage_max_words", &Tuning::node_stage_max_words, 0, 36864, false},
@@ -278,6 +279,14 @@ void Engine::compile() {
                                  1ull << 22, tune, nullptr, true) &&
                 (blob.size() > kStageBlobWords || lc.size() <= kStageBlobWords))
                 blob.swap(lc);
+        }
+        // dst-independent CROSS tables that fit LDS: the fixed-depth form (no dst stream, no
+        // per-lane branches in the walk)
+        bool dst_free = true;  // no rule tests dst (ANY-protocol packets included)
+        for (uint32_t r = 0; r < hdr.n_rules; r++) dst_free &= h.rules[hdr.rule_base + r].dmask == 0;
+        if (ok && tune.fd && an[t] && dst_free) {
+            std::vector<uint32_t> fd;
+            if (build_fd_blob(*an[t], (kActDeny << 30) | (NR + (uint32_t)t), tune, fd, kStageBlobWords)) blob.swap(fd);
         }
         if (ok) {
             while (blob.size() % 4) blob.push_back(0);

@@ -524,6 +524,93 @@ bool build_fast_table(const DevRule* rules, uint32_t n, uint32_t rule_base, uint
     return true;
 }
 
+// ---- FD blob: the fixed-depth form of a dst-independent CROSS table --------------------------
+// Layout (u32 words; entries hold byte offsets, so a blob is < 4 MiB):
+//   [0] kFlagFD  [1] default verdict  [2] src root (16)  [3] s1  [4] key root  [5] k1
+//   [6] depth D (reads per field, root included)  [7] bias = 4 - 4 * KLEAF  [8] n_key_classes
+//   [10] n_src_classes
+//   src trie | key trie (node encoding, blobwalk.hpp node_entry; leaves: pointers to self words)
+//   rows: per src class c, {self word, verdict[c][0 .. nkc-1]}
+//   KLEAF: per key class k, a self word
+// A self word at byte A holds A << 10 (stride 0: reading "its child" reads itself), so every
+// lookup is exactly D reads per field plus one verdict read at
+//   (src self) + 4 + 4 * key class = (src self) + (key self) + bias,
+// with no per-lane branch (fd_walk). Only tables without dst lists qualify: their verdict never
+// depends on the dst address, so the kernel does not read the dst stream for them.
+namespace {
+// depth (reads, root included) of a node-encoded trie rooted at word `root` with 2^s1 entries
+uint32_t node_trie_depth(const std::vector<uint32_t>& b, uint32_t root, uint32_t s1) {
+    uint32_t d = 1;
+    struct J {
+        uint32_t at, n, depth;
+    };
+    std::vector<J> st{{root, 1u << s1, 1}};
+    while (!st.empty()) {
+        J j = st.back();
+        st.pop_back();
+        d = std::max(d, j.depth);
+        for (uint32_t e = 0; e < j.n; e++) {
+            const uint32_t v = b[j.at + e];
+            if (v & kLeaf) continue;
+            st.push_back({(v >> 10) / 4u, 1u << ((v >> 5) & 31u), j.depth + 1});
+        }
+    }
+    return d;
+}
+// leaves (kLeaf | class) of a node-encoded trie -> self-word pointers (word of class c: base + c * step)
+void fd_point_leaves(std::vector<uint32_t>& b, uint32_t root, uint32_t s1, uint32_t base, uint32_t step) {
+    std::vector<std::pair<uint32_t, uint32_t>> st{{root, 1u << s1}};
+    while (!st.empty()) {
+        auto j = st.back();
+        st.pop_back();
+        for (uint32_t e = 0; e < j.second; e++) {
+            uint32_t& v = b[j.first + e];
+            if (v & kLeaf) v = ((base + (v & ~kLeaf) * step) * 4u) << 10;
+            else st.push_back({(v >> 10) / 4u, 1u << ((v >> 5) & 31u)});
+        }
+    }
+}
+}  // namespace
+
+bool build_fd_blob(const TableAnalysis& A, uint32_t dflt, const Tuning& tu, std::vector<uint32_t>& blob,
+                   uint32_t max_words) {
+    if (!A.clist.empty() || A.nsc == 0 || A.nkc == 0) return false;  // dst lists: the verdict reads dst
+    for (bool lc : {true, false}) {
+        blob.assign(16, 0);
+        const uint32_t s1 = std::min<uint32_t>(pick_stride(A.sb.size(), 32, tu), 12u);
+        if (build_trie(blob, A.sb, A.sint_cls, 32, s1, tu, lc, true) != kSrcRoot) continue;
+        const uint32_t k1 = std::min<uint32_t>(pick_stride(A.kb.size(), 18, tu), 12u);
+        const uint32_t kroot = build_trie(blob, A.kb, A.kseg_cls, 18, k1, tu, lc, true);
+        if (kroot == kTrieFail) continue;
+        const uint32_t depth = std::max(node_trie_depth(blob, kSrcRoot, s1), node_trie_depth(blob, kroot, k1));
+        const uint32_t row0 = (uint32_t)blob.size(), rstep = A.nkc + 1;
+        const uint32_t kleaf = row0 + A.nsc * rstep;
+        const uint64_t words = (uint64_t)kleaf + A.nkc;
+        if (words > max_words || words * 4 >= (1u << 22)) continue;
+        fd_point_leaves(blob, kSrcRoot, s1, row0, rstep);
+        fd_point_leaves(blob, kroot, k1, kleaf, 1);
+        blob.resize(words, 0);
+        for (uint32_t c = 0; c < A.nsc; c++) {
+            const uint32_t r = row0 + c * rstep;
+            blob[r] = (r * 4u) << 10;
+            for (uint32_t k = 0; k < A.nkc; k++) blob[r + 1 + k] = A.cverd[(size_t)c * A.nkc + k];
+        }
+        for (uint32_t k = 0; k < A.nkc; k++) blob[kleaf + k] = ((kleaf + k) * 4u) << 10;
+        blob[0] = kFlagFD;
+        blob[1] = dflt;
+        blob[2] = kSrcRoot;
+        blob[3] = s1;
+        blob[4] = kroot;
+        blob[5] = k1;
+        blob[6] = depth;
+        blob[7] = 4u - 4u * kleaf;
+        blob[8] = A.nkc;
+        blob[10] = A.nsc;
+        return true;
+    }
+    return false;
+}
+
 // ---- node classifier -------------------------------------------------------------------------
 // One IPv4 partition for the whole node: cut at every covered table's src interval boundary
 // and around every local pod address; elementary intervals with the same end point
