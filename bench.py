@@ -41,6 +41,10 @@ def parse():
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--config", type=int, default=2, choices=sorted(W.CONFIGS))
     p.add_argument("--tuples", type=int, default=0, help="tuples per GPU (weak scaling; default: the config's)")
+    p.add_argument("--rules", type=int, default=0,
+                   help="config 2 only: rules of the gen-policy-shaped table (rule-count sweep; default 1000)")
+    p.add_argument("--cpu-seconds", type=float, default=10.0,
+                   help="budget of the multithreaded CPU baseline (the sample is sized by a calibration run)")
     p.add_argument("--scaling", choices=("weak", "strong"), default="weak",
                    help="weak: --tuples per GPU; strong: --total-tuples split over the GPUs")
     p.add_argument("--total-tuples", type=int, default=0,
@@ -97,6 +101,10 @@ def main():
     else:
         torch.cuda.set_device(local)
     kw = {"n_tuples": a.tuples} if a.tuples else {}
+    if a.rules:
+        if a.config != 2:
+            raise SystemExit("--rules applies to config 2 (the gen-policy-shaped table)")
+        kw["n_rules"] = a.rules
     w = W.CONFIGS[a.config](local, **kw)
     e = w.engine
     if a.per_table:
@@ -147,12 +155,13 @@ def main():
 
     bpt, fields = bytes_per_tuple(w)
     achieved = n * bpt / (kern_ms * 1e-3) / 1e9
-    traffic, traffic_src = pmc_traffic(a.config, n, a.counters and not w.counters)
+    traffic, traffic_src = pmc_traffic(a.config, n, (a.counters and not w.counters) or bool(a.rules))
     line = {
         "metric": METRIC, "value": round(mpps, 1), "unit": "Mpps", "n_gpus": world, "steps": a.steps,
         "warmup": a.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True, "scaling": a.scaling,
         "vs_baseline": None, "dtype": "u32", "data": "synthetic (device-generated, counter-based splitmix64)",
-        "config": {"workload": "config%d: %s" % (a.config, w.desc), "mode": MODE_NAME[w.mode],
+        "config": {"workload": "config%d: %s" % (a.config, w.desc) + (" [rule-count sweep]" if a.rules else ""),
+                   "mode": MODE_NAME[w.mode],
                    "tuples_per_gpu": n, "tuples_total": total_tuples // a.steps, "rules": st["rules"],
                    "tables": st["tables"], "parallelism": "dp%d" % world,
                    "counters": bool(use_counters), "classifier": classifier(w, a.per_table)},
@@ -164,7 +173,8 @@ def main():
     if allreduce is not None:
         line.update(allreduce)
     if rank == 0 and world == 1 and not a.no_cpu:
-        line["cpu_baseline"], line["parity_sample"] = cpu_baseline(w, b, out, a.cpu_sample, a.faithful_seconds)
+        line["cpu_baseline"], line["parity_sample"] = cpu_baseline(w, b, out, a.cpu_sample, a.faithful_seconds,
+                                                                   a.cpu_seconds)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:
@@ -207,6 +217,8 @@ def dry_run(a, rank, world):
     if world > 1:
         dist.init_process_group("gloo")
     kw = {"n_tuples": a.tuples or 1 << 14}
+    if a.rules:
+        kw["n_rules"] = a.rules
     w = W.CONFIGS[a.config](0, **kw)
     e = w.engine
     base, n = shard_of(a, w, rank, world)
@@ -250,9 +262,9 @@ def bytes_per_tuple(w):
     """Algorithmic bytes per tuple: the tuple fields the classification reads
     plus the 4-B verdict. SINGLE / PERPOD read src 4 + dst 4 + dport 2 + proto 1 = 11 B (15 B
     with the verdict), CONN also sport (17 B) -- except SINGLE over a table no rule of which
-    tests dst (compiled to the FD form): its verdict cannot depend on dst and the kernel does
-    not read that stream, so 7 B in + 4 B out = 11 B."""
-    if w.mode == 0 and w.engine.table_stats(w.table_id)["structure"] == "fd":
+    tests dst (kFlagDstFree; FD tables among them): its verdict cannot depend on dst and the
+    kernel does not read that stream, so 7 B in + 4 B out = 11 B."""
+    if w.mode == 0 and w.engine.table_stats(w.table_id)["dst_free"]:
         return 11, "src 4 + dport 2 + proto 1 in, verdict 4 out (no rule tests dst: dst not read)"
     if w.mode == 2:
         return 17, "src 4 + dst 4 + sport 2 + dport 2 + proto 1 in, verdict 4 out"
@@ -270,7 +282,7 @@ def classifier(w, per_table):
     return "node: %s" % json.dumps(ns)
 
 
-def pmc_traffic(config, n, counters):
+def pmc_traffic(config, n, other_shape):
     """HBM bytes per classify launch from the committed rocprofv3 PMC summary of this config
     (profiles/rNN_*_config<C>_pmc.json, FETCH_SIZE/WRITE_SIZE passes, gfx950-corrected by
     tools/prof_summary.py), scaled to this launch's tuple count; None when there is none."""
@@ -279,27 +291,34 @@ def pmc_traffic(config, n, counters):
     # newest round / version first by number (r01_v12 after r01_v9)
     nat = lambda p: [int(x) if x.isdigit() else x for x in re.split(r"(\d+)", os.path.basename(p))]
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_config%d_pmc.json" % config)), key=nat)
-    if not files or counters:
+    if not files or other_shape:  # the committed summary is of the default shape only
         return None, None
     with open(files[-1]) as f:
         p = json.load(f)
     return int(p["hbm_traffic_bytes_per_launch"] * n / p["tuples_per_launch"]), os.path.basename(files[-1])
 
 
-def cpu_baseline(w, b, out, k, faithful_s=8.0):
+def cpu_baseline(w, b, out, k, faithful_s=8.0, budget_s=10.0):
     """The oracle's evalACL/testConnection (oracle/oracle.c) timed on this host's cores over
-    the first k tuples of the same workload; also checks the GPU verdicts on that sample."""
+    the first k tuples of the same workload (k capped so the run takes about budget_s: a
+    calibration run on 4096 tuples sizes it); also checks the GPU verdicts on that sample."""
     from oracle import fast, world  # cpu_baseline leg: the checker, never the thing measured on GPU
 
-    k = min(k, b.n)
-    src, dst, sport, dport, proto = b.numpy(k)
-    got = out[:k].cpu().numpy().view(np.uint32)
     e = w.engine
     threads = min(16, os.cpu_count() or 1)
+    k = min(k, b.n)
+    if w.mode == 0:
+        ora = fast.OraACL(e.GetACLByName(e.ACLNames()[w.table_id])["rules"])
+        c = min(4096 * threads, k)
+        cs = b.numpy(c)
+        t0 = time.perf_counter()
+        fast.eval_acl(ora, cs[0], cs[1], cs[3], cs[4], threads=threads)
+        k = int(min(k, max(c, c / max(time.perf_counter() - t0, 1e-9) * budget_s)))
+    src, dst, sport, dport, proto = b.numpy(k)
+    got = out[:k].cpu().numpy().view(np.uint32)
     extra = {}
     faithful_ok = None
     if w.mode == 0:
-        ora = fast.OraACL(e.GetACLByName(e.ACLNames()[w.table_id])["rules"])
         t0 = time.perf_counter()
         act, idx = fast.eval_acl(ora, src, dst, dport, proto, threads=threads)
         dt = time.perf_counter() - t0
@@ -310,10 +329,11 @@ def cpu_baseline(w, b, out, k, faithful_s=8.0):
         # reference-faithful variant (CIDR strings parsed per rule visit, one thread): a
         # 4096-tuple calibration run sizes the sample to about faithful_s seconds
         rules = e.GetACLByName(e.ACLNames()[w.table_id])["rules"]
+        cal = 64 if len(rules) > 20000 else 4096
         t0 = time.perf_counter()
-        fast.eval_acl_faithful(rules, src[:4096], dst[:4096], dport[:4096], proto[:4096])
-        rate = 4096 / max(time.perf_counter() - t0, 1e-9)
-        kf = int(min(k, max(4096, rate * faithful_s)))
+        fast.eval_acl_faithful(rules, src[:cal], dst[:cal], dport[:cal], proto[:cal])
+        rate = cal / max(time.perf_counter() - t0, 1e-9)
+        kf = int(min(k, max(cal, rate * faithful_s)))
         t0 = time.perf_counter()
         fa, fi = fast.eval_acl_faithful(rules, src[:kf], dst[:kf], dport[:kf], proto[:kf])
         extra["faithful_1thread_mpps"] = round(kf / (time.perf_counter() - t0) / 1e6, 4)
@@ -335,8 +355,8 @@ def cpu_baseline(w, b, out, k, faithful_s=8.0):
         slot = wd.slots(lt, li)
         kind += ", interfaces resolved beforehand"
     ok = bool(((got >> 30) == act.astype(np.uint32)).all() and ((got & 0x3FFFFFFF) == slot).all())
-    base = {"value": round(k / dt / 1e6, 3), "unit": "Mpps", "cores": threads, "kind": "port",
-            "sample": "first %d tuples of the same workload; %s" % (k, kind)}
+    base = {"value": round(k / dt / 1e6, 3), "unit": "Mpps", "cores": threads, "host_cpus": os.cpu_count(),
+            "kind": "port", "sample": "first %d tuples of the same workload; %s" % (k, kind)}
     base.update(extra)
     parity = {"tuples": k, "bit_exact_action_and_rule_index": ok}
     if faithful_ok is not None:

@@ -283,3 +283,41 @@ def test_rccl_counter_allreduce_single_rank():
     D.classify(e2, MODE_SINGLE, e2.table_id("x"), b, out, counters=D.counters_device_ptr(e2))
     s2 = D.allreduce_counters_all([e2])[0]
     assert int(s2.sum()) == b.n
+
+
+# ---- rule-count sweep: gen-policy-shaped tables of 10k / 100k rules and the whole policy ----
+@pytest.mark.parametrize("n_rules", [10000, 100000])
+def test_rule_count_sweep_tables_bit_exact(n_rules):
+    """config 2's shape at 10k and 100k rules: FD blobs too large for LDS (prefix staged,
+    STAGE 5; and the generic walk with nothing staged), with and without counters."""
+    w = W.config2(0, n_tuples=2 << 20, n_rules=n_rules)
+    assert w.engine.table_stats(w.table_id)["structure"] == "fd"
+    b = D.TupleBatch(w.n_tuples, with_sport=False)
+    D.gen_tuples(w.engine, b, **w.gen)
+    torch.cuda.synchronize()
+    src, dst, sport, dport, proto = b.numpy(b.n)
+    act, slot, rules = _expected_single(w, src, dst, dport, proto)
+    for tune in ({}, {"stage_root_max_words": 0}):
+        for counters in (False, True):
+            got, cnt = _classify(w, b, counters=counters, **tune)
+            assert np.array_equal(got >> 30, act) and np.array_equal(got & 0x3FFFFFFF, slot), (tune, counters)
+            if counters:
+                assert np.array_equal(cnt, np.bincount(slot, minlength=len(cnt)))
+    assert len(np.unique(slot)) > n_rules // 4
+
+
+def test_full_gen_policy_through_configurator():
+    """config 7: the whole gen-policy.py policy (1000 CIDRs x 5 excepts x 20 ports, both
+    directions) through the configurator; the pod's ~466k-rule table classified on the GPU
+    and checked against the oracle on a sample."""
+    w = W.config7(0, n_tuples=1 << 20)
+    e = w.engine
+    assert e.table_info(w.table_id)[1] > 400000
+    b = D.TupleBatch(w.n_tuples, with_sport=False)
+    D.gen_tuples(e, b, **w.gen)
+    got, _ = _classify(w, b)
+    k = 131072
+    src, dst, sport, dport, proto = b.numpy(k)
+    act, slot, _ = _expected_single(w, src, dst, dport, proto)
+    assert np.array_equal(got[:k] >> 30, act) and np.array_equal(got[:k] & 0x3FFFFFFF, slot)
+    assert len(np.unique(act)) == 2

@@ -24,6 +24,9 @@ constexpr uint32_t kFlagCross = 1u, kFlagLists = 2u, kFlagCand = 4u, kFlagLinear
 // depend on the dst address, laid out so that every lookup is exactly D dependent reads per
 // field and one verdict read, with no per-lane branches (fd_walk below).
 constexpr uint32_t kFlagFD = 32u;
+// no rule of the table tests dst (set by engine.cpp in DevTable::fsk, not in the blob): SINGLE
+// launches do not read the dst stream
+constexpr uint32_t kFlagDstFree = 64u;
 constexpr uint32_t kPairHdr = 12u;  // PAIR blob header words: dst root, d1, pair table, n_dst_classes
 constexpr uint32_t kLeaf = 0x80000000u;
 // non-leaf trie entry: child block offset (words) | child stride << kTrieStrideShift
@@ -210,32 +213,42 @@ PG_HD void blob_walk(const L (&ld)[Q], const BlobTab (&tb)[Q], const bool (&on)[
     blob_walk<PRED>(ld, ld, tb, on, src, dst, key, w);
 }
 
-// FD blob walk (layout: fastpath.cpp build_fd_blob). Tries in the node encoding (non-leaf
-// entry = child byte offset << 10 | stride << 5 | shift); a leaf is a pointer to a word that
-// points to itself (stride 0), so a finished lookup re-reads that word and every lookup takes
-// the same D reads: src -> the self word heading its src class's verdict row, key -> the self
-// word of its key class. Verdict = the word at (src self) + (key self) + bias, i.e. row[1 +
-// key class]. fsk: s1 << 8 | k1 << 16; kroot: key trie root (words); depth: reads per field;
-// bias: 4 - 4 * (first key self word). ld must provide at_byte.
-template <class L, int Q>
-PG_HD void fd_walk(const L& ld, uint32_t fsk, uint32_t kroot, uint32_t depth, uint32_t bias, const uint32_t (&src)[Q],
-                   const uint32_t (&key)[Q], uint32_t (&w)[Q]) {
+// FD blob walk (layout: fastpath.cpp build_fd_blob). Tries in the kEncWords encoding
+// (non-leaf entry = child WORD offset << 10 | stride << 5 | shift of the child level); a leaf is
+// a pointer to a word that points to itself (stride 0), so a finished lookup re-reads that
+// word and every lookup takes the same D reads: src -> the self word heading its src class's
+// verdict row, key -> the self word of its key class. Verdict = the word at (src self) +
+// (key self) + bias, i.e. row[1 + key class]. fsk: s1 << 8 | k1 << 16; kroot: key trie root;
+// depth: reads per field; bias: 1 - (first key self word).
+// lp reads the blob's prefix (header, src root, key trie and self words: the LDS copy when a
+// launch stages only that), lb everything else (the src levels below the root and the rows).
+PG_HD uint32_t fd_child(uint32_t e, uint32_t a) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return (e >> 10) + __builtin_amdgcn_ubfe(a, e, e >> 5);
+#else
+    const uint32_t w = (e >> 5) & 31u;
+    return (e >> 10) + ((a >> (e & 31u)) & ((1u << w) - 1u));
+#endif
+}
+template <class LP, class LB, int Q>
+PG_HD void fd_walk(const LP& lp, const LB& lb, uint32_t fsk, uint32_t kroot, uint32_t depth, uint32_t bias,
+                   const uint32_t (&src)[Q], const uint32_t (&key)[Q], uint32_t (&w)[Q]) {
     const uint32_t ss = 32u - ((fsk >> 8) & 0xFFu), sk = 18u - ((fsk >> 16) & 0xFFu);
     uint32_t es[Q], ek[Q];
     PG_UNROLL
     for (int j = 0; j < Q; j++) {
-        es[j] = ld.at_byte(4u * kSrcRoot + ((src[j] >> ss) << 2));
-        ek[j] = ld.at_byte(4u * kroot + ((key[j] >> sk) << 2));
+        es[j] = lp.u32(kSrcRoot + (src[j] >> ss));
+        ek[j] = lp.u32(kroot + (key[j] >> sk));
     }
     for (uint32_t l = 1; l < depth; l++) {
         PG_UNROLL
         for (int j = 0; j < Q; j++) {
-            es[j] = ld.at_byte(node_child_byte(es[j], src[j]));
-            ek[j] = ld.at_byte(node_child_byte(ek[j], key[j]));
+            es[j] = lb.u32(fd_child(es[j], src[j]));
+            ek[j] = lp.u32(fd_child(ek[j], key[j]));
         }
     }
     PG_UNROLL
-    for (int j = 0; j < Q; j++) w[j] = ld.at_byte((es[j] >> 10) + (ek[j] >> 10) + bias);
+    for (int j = 0; j < Q; j++) w[j] = lb.u32((es[j] >> 10) + (ek[j] >> 10) + bias);
 }
 
 struct HostLoader {

@@ -476,7 +476,8 @@ int pg_debug_walk_blob(pg_ctx* ctx, const char* acl_name, const uint32_t* src, c
         for (uint64_t i = 0; i < n; i++) {
             const uint32_t s1[1] = {src[i]}, dp1[1] = {dst_port[i]}, pr1[1] = {proto[i]};
             uint32_t w1[1];
-            classify_fd_q<false, 1>(T, E.host.blobs.data() + hd.blob_off, hd, s1, dp1, pr1, Hist{nullptr, nullptr}, w1);
+            const uint32_t* b = E.host.blobs.data() + hd.blob_off;
+            classify_fd_q<false, 1>(T, b, b, hd, s1, dp1, pr1, Hist{nullptr, nullptr}, w1);
             out[i] = w1[0];
         }
         return PG_OK;
@@ -552,6 +553,9 @@ DevTableSet host_view(const HostTableSet& h) {
     v.node = h.node;
     v.node.img = h.node_img.empty() ? nullptr : h.node_img.data();
     v.node.cross = h.node_img.empty() ? nullptr : h.node_cross.data();
+    v.host_tabs = h.tabs.data();
+    v.host_blob_words = h.blob_words.data();
+    v.host_blob_prefix = h.blob_prefix.data();
     return v;
 }
 

@@ -33,6 +33,9 @@ namespace pg {
 #ifndef PG_NODE_FB_Q1  // node kernels: per-table fallback one tuple at a time
 #define PG_NODE_FB_Q1 1
 #endif
+#ifndef PG_NODE_FB_CALL  // node kernels: that fallback is an out-of-line call (keeps it out of
+#define PG_NODE_FB_CALL 1  // the hot loop's code and register allocation)
+#endif
 
 // TCP -> port, UDP -> 0x10000 | port, OTHER -> 0x20000, anything else -> 0x30000 (branch-free)
 PG_HD uint32_t pkt_key(uint32_t proto, uint32_t port) {
@@ -130,7 +133,7 @@ PG_HD void eval_q(const DevTableSet& T, const uint32_t* blobs, const DevTable (&
             if (!fd[j]) continue;
             const uint32_t s1[1] = {src[j]}, k1[1] = {key[j]};
             uint32_t w1[1];
-            fd_walk(ld[j], tab[j].fsk, tab[j].kroot, tab[j].xoff, tab[j].nkc, s1, k1, w1);
+            fd_walk(ld[j], ld[j], tab[j].fsk, tab[j].kroot, tab[j].xoff, tab[j].nkc, s1, k1, w1);
             w[j] = w1[0];
         }
     }
@@ -138,6 +141,30 @@ PG_HD void eval_q(const DevTableSet& T, const uint32_t* blobs, const DevTable (&
     for (int j = 0; j < Q; j++)
         if (act[j] && ((!on[j] && !fd[j]) || key[j] >= kWalkKeyLimit))
             w[j] = eval_linear(T.rules, tab[j].rule_base, tab[j].n_rules, tab[j].dflt, src[j], dst[j], key[j]);
+}
+
+// evalACL of one tuple against one table by its per-table blob (and the linear scan for LINEAR
+// tables and ANY-protocol keys): the node kernels' rare fallback, out of line on the device.
+// Scalar arguments only, so the call needs no stack frame for them.
+PG_NOINLINE uint32_t eval_one(const DevRule* rules, const uint32_t* blobs, const DevTable* tabs, int32_t t,
+                              uint32_t src, uint32_t dst, uint32_t key) {
+    const DevTable tab = load_tab(tabs, t);
+    if (tab.fsk & kFlagFD) {
+        const uint32_t s1[1] = {src}, k1[1] = {key};
+        uint32_t w1[1];
+        const DevLoader ld{blobs + tab.blob_off};
+        fd_walk(ld, ld, tab.fsk, tab.kroot, tab.xoff, tab.nkc, s1, k1, w1);
+        if (key < kWalkKeyLimit) return w1[0];
+    } else if (!(tab.fsk & kFlagLinear) && key < kWalkKeyLimit) {
+        const DevLoader ld[1] = {DevLoader{blobs + tab.blob_off}};
+        const BlobTab tb[1] = {BlobTab{tab.fsk, tab.dflt, tab.kroot, tab.xoff, tab.nkc}};
+        const bool on[1] = {true};
+        const uint32_t s1[1] = {src}, d1[1] = {dst}, k1[1] = {key};
+        uint32_t w1[1];
+        blob_walk(ld, tb, on, s1, d1, k1, w1);
+        return w1[0];
+    }
+    return eval_linear(rules, tab.rule_base, tab.n_rules, tab.dflt, src, dst, key);
 }
 
 // tables of a connection end point: interface (-1/-2 unresolvable) and its ACLs
@@ -216,17 +243,19 @@ struct Hist {
     }
 };
 
-// SINGLE mode over an FD table (uniform: tab0), its blob at `blob` (the LDS copy in the kernels):
-// Q tuples per lane, fixed-depth walks in lockstep; ANY-protocol packets take the linear scan.
+// SINGLE mode over an FD table (uniform: tab0): Q tuples per lane, fixed-depth walks in
+// lockstep; ANY-protocol packets take the linear scan. prefix: the blob's prefix (its LDS copy
+// in the kernels), blob: the whole blob (the same LDS copy when it is staged whole, else HBM).
 // The dst address is not an input: no rule of an FD table tests it (engine.cpp compile).
 template <bool COUNT, int Q>
-PG_HD void classify_fd_q(const DevTableSet& T, const uint32_t* blob, const DevTable& tab0, const uint32_t (&s)[Q],
-                         const uint32_t (&dp)[Q], const uint32_t (&pr)[Q], const Hist& h, uint32_t (&out)[Q]) {
+PG_HD void classify_fd_q(const DevTableSet& T, const uint32_t* prefix, const uint32_t* blob, const DevTable& tab0,
+                         const uint32_t (&s)[Q], const uint32_t (&dp)[Q], const uint32_t (&pr)[Q], const Hist& h,
+                         uint32_t (&out)[Q]) {
     uint32_t key[Q];
     bool any = false;
     PG_UNROLL
     for (int j = 0; j < Q; j++) key[j] = pkt_key(pr[j], dp[j]), any |= key[j] >= kWalkKeyLimit;
-    fd_walk(DevLoader{blob}, tab0.fsk, tab0.kroot, tab0.xoff, tab0.nkc, s, key, out);
+    fd_walk(DevLoader{prefix}, DevLoader{blob}, tab0.fsk, tab0.kroot, tab0.xoff, tab0.nkc, s, key, out);
     if (any) {
         PG_UNROLL
         for (int j = 0; j < Q; j++)  // no rule of an FD table tests dst (engine.cpp): any dst will do
@@ -485,8 +514,14 @@ struct NodeEval {
         bool anyfb = false;
         PG_UNROLL
         for (int j = 0; j < Q; j++) anyfb |= fb[j];
+#if defined(PG_PROBE_NOFB)  // measurement build only: the per-table fallback compiled out
+        anyfb = false;
+#endif
         if (anyfb) {
-#if PG_NODE_FB_Q1
+#if PG_NODE_FB_CALL
+            for (int j = 0; j < Q; j++)
+                if (fb[j]) w[j] = eval_one(T.rules, T.blobs, T.tabs, t[j], a[j], b[j], k[j]);
+#elif PG_NODE_FB_Q1
             // the per-table path one tuple at a time: it is rare here (tables the node does
             // not cover, ANY-protocol packets), and a lockstep walk of Q tuples would size the
             // whole kernel's register allocation

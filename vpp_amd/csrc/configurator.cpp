@@ -6,10 +6,7 @@
 namespace pg {
 
 bool ContivRules::insert(const ContivRule& r) {  // configurator_impl.go:520-540
-    auto it = std::partition_point(ordered.begin(), ordered.end(),
-                                   [&](const ContivRule& x) { return r.compare(x) > 0; });
-    if (it != ordered.end() && r.compare(*it) == 0) return false;
-    ordered.insert(it, r);
+    if (!ordered.insert(r).second) return false;  // Compare == 0 with a rule already in
     rules.push_back(r);
     return true;
 }

@@ -11,6 +11,7 @@
 //   utils.GetOneHostSubnet(FromIP)                          plugins/policy/utils/utils.go:270-291
 //   MockRenderer (NewTxn / Render / Commit / TestTraffic)   mock/renderer/renderer_mock.go:39-185
 #pragma once
+#include <set>
 #include <functional>
 #include <map>
 #include <memory>
@@ -49,8 +50,15 @@ struct CfgPolicy {
 using CfgPolicies = std::vector<std::shared_ptr<const CfgPolicy>>;
 
 // ContivRules: insertion order (what renderers receive) + ordered set (deduplication)
+// The reference keeps a sorted slice for dedup (binary search + O(n) shift per insert); a set
+// under the same total order gives the same answers in O(log n), which matters for policies
+// with ~500k rules (tests/policy/perf/gen-policy.py's shape).
+struct RuleLess {
+    bool operator()(const ContivRule& a, const ContivRule& b) const { return a.compare(b) < 0; }
+};
 struct ContivRules {
-    std::vector<ContivRule> ordered, rules;
+    std::set<ContivRule, RuleLess> ordered;
+    std::vector<ContivRule> rules;  // in insertion order (CopySlice)
     bool insert(const ContivRule& r);
 };
 

@@ -42,7 +42,7 @@ struct DeviceBuffers {
     void* blob = nullptr;
     DevTableSet view{};
     std::vector<DevTable> host_tabs;
-    std::vector<uint32_t> host_blob_words;
+    std::vector<uint32_t> host_blob_words, host_blob_prefix;
     // streams that launched kernels reading this set, with an event recorded after the last
     // launch on each: the set is freed (and counters read) once those have completed, without
     // a device-wide synchronisation
@@ -168,8 +168,10 @@ DeviceBuffers* dev_upload(const HostTableSet& h, std::string* err) {
     v.node.cross = h.node_img.empty() ? nullptr : (const uint32_t*)(base + o_nx);
     b->host_tabs = h.tabs;
     b->host_blob_words = h.blob_words;
+    b->host_blob_prefix = h.blob_prefix;
     v.host_tabs = b->host_tabs.data();
     v.host_blob_words = b->host_blob_words.data();
+    v.host_blob_prefix = b->host_blob_prefix.data();
     return b;
 }
 
@@ -323,7 +325,9 @@ __device__ __forceinline__ void stream_store(V v, V* p) {
 // blob too large for LDS has its header and src-trie root (stage_words) copied, so the first
 // dependent load of every lookup hits LDS and the rest read HBM / L2; 4 = an FD blob
 // (fastpath.cpp build_fd_blob) staged like 1 and walked by classify_fd_q: fixed-depth reads,
-// no per-lane branches, and no dst stream (no rule of an FD table tests dst).
+// no per-lane branches, and no dst stream (no rule of an FD table tests dst); 5 = an FD blob
+// too large for LDS: its prefix (header, src root, key trie) staged, the src levels below the
+// root and the verdict rows read from HBM / L2.
 // NODE (PERPOD / CONN): the node classifier; STAGE then copies the node image into LDS.
 //
 // Stream pipelining (PG_PREFETCH): 1 = the next group's loads are issued at the top of each
@@ -350,8 +354,8 @@ __device__ __forceinline__ void stream_store(V v, V* p) {
 #ifndef PG_QSINGLE
 #define PG_QSINGLE 2
 #endif
-#ifndef PG_QPOD
-#define PG_QPOD 4
+#ifndef PG_QPOD  // PERPOD: 2 (A/B on MI355X, config 3: 237 vs 198 Gpps at 4 -- fewer registers)
+#define PG_QPOD 2
 #endif
 #ifndef PG_QCONN
 #define PG_QCONN 1
@@ -362,7 +366,10 @@ __device__ __forceinline__ void stream_store(V v, V* p) {
 #ifndef PG_QSINGLE_FD  // SINGLE over an LDS-staged FD table (STAGE 4)
 #define PG_QSINGLE_FD 1
 #endif
-#ifndef PG_PREFETCH_FD  // STAGE 4: stream prefetch of the next group (see PG_PREFETCH)
+#ifndef PG_QSINGLE_FDG  // SINGLE over an FD table read from HBM, its prefix staged (STAGE 5)
+#define PG_QSINGLE_FDG 2
+#endif
+#ifndef PG_PREFETCH_FD  // STAGE 4 / 5: stream prefetch of the next group (see PG_PREFETCH)
 #define PG_PREFETCH_FD 0
 #endif
 #ifndef PG_TPL  // tuples per lane per loop iteration (4 or 8)
@@ -400,7 +407,9 @@ __device__ __forceinline__ void st_words(const Words<NW>& v, uint32_t* p) {
 #ifndef PG_NODE_WPE  // node kernels: minimum waves per SIMD the register allocation must allow (1 = any)
 #define PG_NODE_WPE 1
 #endif
-template <int MODE, bool COUNT, bool VEC, int STAGE, bool NODE, int BS>
+// STAGE_ + 8 (SINGLE, STAGE 0-2): the table is dst-free (kFlagDstFree: no rule tests dst), so
+// the dst stream is not read
+template <int MODE, bool COUNT, bool VEC, int STAGE_, bool NODE, int BS>
 __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(NODE ? PG_NODE_WPE : 1)))
 void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
                                                      const uint32_t* __restrict__ dst,
@@ -409,6 +418,8 @@ void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
                                                      const uint8_t* __restrict__ proto, uint64_t n,
                                                      uint32_t* __restrict__ out, unsigned long long* counters,
                                                      uint32_t stage_words) {
+    constexpr int STAGE = STAGE_ & 7;
+    constexpr bool NODST = MODE == 0 && STAGE_ >= 8;
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     uint32_t* hist = smem + (STAGE ? stage_words : 0u);
     Hist h{nullptr, counters};
@@ -426,7 +437,7 @@ void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
         if (STAGE) {
             const uint4* g = reinterpret_cast<const uint4*>(T.blobs + tab0.blob_off);
             for (uint32_t i = threadIdx.x; i < stage_words / 4u; i += BS) reinterpret_cast<uint4*>(smem)[i] = g[i];
-            if (STAGE == 1 || STAGE == 4) {
+            if (STAGE == 1 || STAGE == 4) {  // (STAGE 5: the prefix in LDS, the rest read from HBM)
                 blobs = smem;
                 tab0.blob_off = 0;
             }
@@ -451,8 +462,10 @@ void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
         Words<P / 2> dp, sp;
         Words<P / 4> pr;
     };
-    // STAGE 4 (SINGLE over an FD table): no rule tests dst, so the dst stream is not read
-    constexpr bool NEED_DST = !(MODE == 0 && STAGE == 4);
+    // STAGE 4 / 5 (SINGLE over an FD table): no rule tests dst, so the dst stream is not read
+    constexpr bool FD = MODE == 0 && (STAGE == 4 || STAGE == 5);
+    constexpr bool NEED_DST = !FD && !NODST;
+    const uint32_t* fd_blob = FD ? (STAGE == 4 ? smem : T.blobs + tab0.blob_off) : nullptr;
     auto load = [&](uint64_t q) {
         Group x;
         const uint64_t i0 = q * P;
@@ -467,7 +480,7 @@ void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
     };
     uint64_t q = first;
     Group cur;
-    constexpr int PF = STAGE == 4 ? PG_PREFETCH_FD : (PG_PREFETCH >= 0 ? PG_PREFETCH : (MODE == 0 ? 0 : 1));
+    constexpr int PF = FD ? PG_PREFETCH_FD : (PG_PREFETCH >= 0 ? PG_PREFETCH : (MODE == 0 ? 0 : 1));
     if (PF && q < nfull) cur = load(q);
     while (q < nfull) {
         const uint64_t qn = q + stride;
@@ -494,7 +507,7 @@ void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
         // lane, more waves per SIMD)
         constexpr int QC = MODE == 2 ? (COUNT ? PG_QCONN_COUNT : PG_QCONN)
                                      : (MODE == 1 ? PG_QPOD
-                                                  : (STAGE == 4 ? PG_QSINGLE_FD
+                                                  : (FD ? (STAGE == 4 ? PG_QSINGLE_FD : PG_QSINGLE_FDG)
                                                                 : (STAGE == 1 ? PG_QSINGLE_LDS : PG_QSINGLE)));
 #pragma unroll
         for (int c = 0; c < P; c += QC) {
@@ -502,8 +515,8 @@ void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
 #pragma unroll
             for (int j = 0; j < QC; j++)
                 cs[j] = sv[c + j], cd[j] = dv[c + j], csp[j] = spv[c + j], cdp[j] = dpv[c + j], cpr[j] = prv[c + j];
-            if constexpr (MODE == 0 && STAGE == 4) {
-                classify_fd_q<COUNT, QC>(T, smem, tab0, cs, cdp, cpr, h, co);
+            if constexpr (FD) {
+                classify_fd_q<COUNT, QC>(T, smem, fd_blob, tab0, cs, cdp, cpr, h, co);
             } else if constexpr (NODE) {
                 if (c == 0)
                     classify_node_q<MODE, COUNT, QC, STAGE && PG_PRED, STAGE == 3>(T, T.node, img, cs, cd, csp, cdp, cpr, h, co, hook);
@@ -528,7 +541,7 @@ void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
         const uint32_t s1[1] = {src[i]}, d1[1] = {NEED_DST ? dst[i] : 0u},
                        sp1[1] = {MODE == 2 ? (uint32_t)sport[i] : 0u}, dp1[1] = {dport[i]}, pr1[1] = {proto[i]};
         uint32_t o[1];
-        if constexpr (MODE == 0 && STAGE == 4) classify_fd_q<COUNT, 1>(T, smem, tab0, s1, dp1, pr1, h, o);
+        if constexpr (FD) classify_fd_q<COUNT, 1>(T, smem, fd_blob, tab0, s1, dp1, pr1, h, o);
         else if constexpr (NODE) classify_node_q<MODE, COUNT, 1, STAGE && PG_PRED, STAGE == 3>(T, T.node, img, s1, d1, sp1, dp1, pr1, h, o);
         else classify_q<MODE, COUNT, 1, STAGE == 1 && PG_PRED>(T, blobs, tab0, s1, d1, sp1, dp1, pr1, h, o, rootb);
         out[i] = o[0];
@@ -725,7 +738,7 @@ static void launch_one(const DevTableSet& T, const Tuning& tu, int t, const uint
         // 512 (A/B on MI355X: SINGLE with counters +14 % over 1024 at config 2; without
         // counters +2.5 % since SINGLE classifies one tuple per chunk, v15), except SINGLE
         // without counters over an HBM blob with its root staged: 1024 (config 4 +1.3 %)
-        const uint32_t bs = tu.block_stage ? tu.block_stage : (MODE == 0 && !COUNT && STAGE == 2 ? 1024u : 512u);
+        const uint32_t bs = tu.block_stage ? tu.block_stage : (MODE == 0 && !COUNT && (STAGE & 7) == 2 ? 1024u : 512u);
         if (bs == 1024u)
             return launch_bs<MODE, COUNT, VEC, STAGE, NODE, 1024>(T, tu, t, src, dst, sport, dport, proto, n, out,
                                                                   counters, st, hist, stage, items);
@@ -735,6 +748,25 @@ static void launch_one(const DevTableSet& T, const Tuning& tu, int t, const uint
     }
     launch_bs<MODE, COUNT, VEC, STAGE, NODE, 256>(T, tu, t, src, dst, sport, dport, proto, n, out, counters, st, hist,
                                                   stage, items);
+}
+
+// SINGLE over a non-FD table: the blob in LDS (STAGE 1), its root in LDS (2) or all in HBM (0);
+// NODST = 8 for dst-free tables
+template <int MODE, bool COUNT, bool VEC, int NODST>
+static void launch_generic(const DevTableSet& T, const Tuning& tu, int t, const uint32_t* src, const uint32_t* dst,
+                           const uint16_t* sport, const uint16_t* dport, const uint8_t* proto, uint64_t n,
+                           uint32_t* out, unsigned long long* counters, hipStream_t st, size_t hist, uint32_t words,
+                           uint32_t root_words, uint64_t items) {
+    const DevTable& hd = T.host_tabs[t];
+    if (!(hd.fsk & kFlagLinear) && words && words <= tu.stage_max_words)
+        launch_one<MODE, COUNT, VEC, 1 + NODST, false>(T, tu, t, src, dst, sport, dport, proto, n, out, counters, st,
+                                                       hist, words, items);
+    else if (!(hd.fsk & kFlagLinear) && words && root_words <= tu.stage_root_max_words)
+        launch_one<MODE, COUNT, VEC, 2 + NODST, false>(T, tu, t, src, dst, sport, dport, proto, n, out, counters, st,
+                                                       hist, root_words, items);
+    else
+        launch_one<MODE, COUNT, VEC, 0 + NODST, false>(T, tu, t, src, dst, sport, dport, proto, n, out, counters, st,
+                                                       hist, 0, items);
 }
 
 template <int MODE, bool COUNT, bool VEC>
@@ -747,18 +779,19 @@ static void launch_classify(const DevTableSet& T, const Tuning& tu, int t, const
         const DevTable& hd = T.host_tabs[t];
         const uint32_t words = T.host_blob_words[t];
         const uint32_t root_words = (kSrcRoot + (1u << ((hd.fsk >> 8) & 0xFFu)) + 3u) & ~3u;
+        const uint32_t prefix = T.host_blob_prefix[t];
         if ((hd.fsk & kFlagFD) && words <= tu.stage_max_words)  // FD blob in LDS, no dst stream
             launch_one<MODE, COUNT, VEC, 4, false>(T, tu, t, src, dst, sport, dport, proto, n, out, counters, st, hist,
                                                    words, items);
-        else if (!(hd.fsk & kFlagLinear) && words && words <= tu.stage_max_words)
-            launch_one<MODE, COUNT, VEC, 1, false>(T, tu, t, src, dst, sport, dport, proto, n, out, counters, st, hist,
-                                                   words, items);
-        else if (!(hd.fsk & kFlagLinear) && words && root_words <= tu.stage_root_max_words)
-            launch_one<MODE, COUNT, VEC, 2, false>(T, tu, t, src, dst, sport, dport, proto, n, out, counters, st, hist,
-                                                   root_words, items);
+        else if ((hd.fsk & kFlagFD) && prefix <= tu.stage_root_max_words)  // its prefix in LDS, the rest in HBM
+            launch_one<MODE, COUNT, VEC, 5, false>(T, tu, t, src, dst, sport, dport, proto, n, out, counters, st, hist,
+                                                   prefix, items);
+        else if (hd.fsk & kFlagDstFree)  // no rule tests dst: the dst stream is not read
+            launch_generic<MODE, COUNT, VEC, 8>(T, tu, t, src, dst, sport, dport, proto, n, out, counters, st, hist,
+                                                words, root_words, items);
         else
-            launch_one<MODE, COUNT, VEC, 0, false>(T, tu, t, src, dst, sport, dport, proto, n, out, counters, st, hist,
-                                                   0, items);
+            launch_generic<MODE, COUNT, VEC, 0>(T, tu, t, src, dst, sport, dport, proto, n, out, counters, st, hist,
+                                                words, root_words, items);
     } else if (tu.node_path && T.node.img) {
         // the image with its common-row section when that fits the LDS budget next to the
         // histogram, else the base image (STAGE 1), else the image is read from HBM / L2

@@ -85,6 +85,7 @@ struct DevTableSet {       // device pointers (valid on the GPU)
     DevNode node;
     const DevTable* host_tabs;       // host copies (launch decisions; not dereferenced on the GPU)
     const uint32_t* host_blob_words;
+    const uint32_t* host_blob_prefix;  // FD blobs: words of the prefix a STAGE 5 launch stages
 };
 
 // Host image of a table set, produced by the compiler and uploaded as one blob.
@@ -92,6 +93,7 @@ struct HostTableSet {
     std::vector<DevRule> rules;
     std::vector<DevTable> tabs;
     std::vector<uint32_t> blob_words;  // per table (0 = linear)
+    std::vector<uint32_t> blob_prefix; // per table: FD blob prefix words (0 = not FD)
     std::vector<uint32_t> blobs;
     std::vector<int32_t> ifaces;
     std::vector<uint32_t> iphash;
@@ -120,6 +122,7 @@ struct Tuning {
     uint32_t lc_node = 0;          // level-compressed node IPv4 trie
     uint32_t node_common = 1;      // common-row section of node images
     uint32_t fd = 1;               // FD form of dst-independent CROSS tables that fit LDS
+    uint32_t cross_max_rules = 1u << 20;  // CROSS (cross product) considered up to this many rules (within budget)
     // launches
     uint32_t blocks_per_cu = 0;    // cap on resident workgroups per CU (0 = occupancy)
     uint32_t stage_max_words = kStageBlobWords;  // table blobs staged whole in LDS
@@ -144,9 +147,10 @@ bool build_fast_table(const DevRule* rules, uint32_t n, uint32_t rule_base, uint
                       TableAnalysis** an = nullptr, bool lc = false);
 void free_analysis(TableAnalysis* an);
 // fastpath.cpp: the FD (fixed-depth, dst-independent) form of a CROSS table without dst lists,
-// when it fits max_words (false otherwise; blobwalk.hpp fd_walk)
+// when it fits max_words (false otherwise; blobwalk.hpp fd_walk); a shape that fits lds_words
+// (the kernel then stages it whole) is preferred over fewer levels
 bool build_fd_blob(const TableAnalysis& an, uint32_t dflt, const Tuning& tu, std::vector<uint32_t>& blob,
-                   uint32_t max_words);
+                   uint32_t max_words, uint32_t lds_words);
 // fastpath.cpp: the node classifier over the tables with an analysis (null = not covered).
 // pods: {IPv4, interface, inbound table, outbound table} of local pods; node_end: the same for
 // every other address. false = over budget (h.node_img left empty).

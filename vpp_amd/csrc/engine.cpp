@@ -35,6 +35,7 @@ const Knob kKnobs[] = {
     {"lc_node", &Tuning::lc_node, 0, 1, true},
     {"node_common", &Tuning::node_common, 0, 1, true},
     {"fd", &Tuning::fd, 0, 1, true},
+    {"cross_max_rules", &Tuning::cross_max_rules, 0, 1 << 24, true},
     {"blocks_per_cu", &Tuning::blocks_per_cu, 0, 64, false},
     {"stage_max_words", &Tuning::stage_max_words, 0, 36864, false},
     {"node_stage_max_words", &Tuning::node_stage_max_words, 0, 36864, false},
@@ -265,6 +266,7 @@ void Engine::compile() {
     }
     const uint32_t NR = (uint32_t)h.rules.size();
     h.blob_words.assign(h.tabs.size(), 0);
+    h.blob_prefix.assign(h.tabs.size(), 0);
     std::vector<TableAnalysis*> an(h.tabs.size(), nullptr);
     for (size_t t = 0; t < h.tabs.size(); t++) {
         DevTable& hdr = h.tabs[t];
@@ -280,18 +282,21 @@ void Engine::compile() {
                 (blob.size() > kStageBlobWords || lc.size() <= kStageBlobWords))
                 blob.swap(lc);
         }
-        // dst-independent CROSS tables that fit LDS: the fixed-depth form (no dst stream, no
-        // per-lane branches in the walk)
+        // dst-independent CROSS tables: the fixed-depth form (no dst stream, no per-lane
+        // branches in the walk); staged whole in LDS when it fits, else its prefix
         bool dst_free = true;  // no rule tests dst (ANY-protocol packets included)
         for (uint32_t r = 0; r < hdr.n_rules; r++) dst_free &= h.rules[hdr.rule_base + r].dmask == 0;
         if (ok && tune.fd && an[t] && dst_free) {
             std::vector<uint32_t> fd;
-            if (build_fd_blob(*an[t], (kActDeny << 30) | (NR + (uint32_t)t), tune, fd, kStageBlobWords)) blob.swap(fd);
+            if (build_fd_blob(*an[t], (kActDeny << 30) | (NR + (uint32_t)t), tune, fd, 1u << 22, tune.stage_max_words)) {
+                blob.swap(fd);
+                h.blob_prefix[t] = blob[9];
+            }
         }
         if (ok) {
             while (blob.size() % 4) blob.push_back(0);
             hdr.blob_off = (uint32_t)h.blobs.size();
-            hdr.fsk = blob[0] | (blob[3] << 8) | (blob[5] << 16);
+            hdr.fsk = blob[0] | (blob[3] << 8) | (blob[5] << 16) | (dst_free ? kFlagDstFree : 0u);
             hdr.kroot = blob[4];
             hdr.xoff = blob[6];
             hdr.nkc = blob[7];

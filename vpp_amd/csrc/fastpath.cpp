@@ -72,11 +72,18 @@ constexpr uint32_t kTrieFail = 0xFFFFFFFFu;
 // Tuning::lc_max_stride: widest stride level compression may pick (A/B on MI355X, config 4:
 // 16 = +4 % over 18, 12 = -3 %)
 constexpr uint32_t kLcRootBits = 14;  // HBM-resident blobs: the root alone is staged in LDS (64 KiB)
-// `node`: the node image's encoding (blobwalk.hpp node_child): a non-leaf entry holds the
-// child's BYTE offset << 10 | stride << 5 | the address shift of the child level, so a step is
-// one bit-field extract and one shifted add; children must lie below 2 MiB.
+// enc: kEncBlob (blobwalk.hpp trie_child / trie_stride); kEncNode, the node image's encoding
+// (blobwalk.hpp node_child): a non-leaf entry holds the child's BYTE offset << 10 | stride << 5
+// | the address shift of the child level, so a step is one bit-field extract and one shifted
+// add, children below 2 MiB; kEncWords, the FD blobs' (blobwalk.hpp fd_walk): the same with
+// the child's WORD offset, children below 16 MiB.
+enum TrieEnc { kEncBlob = 0, kEncNode = 1, kEncWords = 2 };
+constexpr uint32_t kWordsChildMax = 1u << 22;
+// cstride: the stride of the levels below the root without level compression (8; FD blobs
+// that must fit LDS try 6 and 4: more, smaller levels)
 uint32_t build_trie(std::vector<uint32_t>& blob, const std::vector<uint64_t>& bnd, const std::vector<uint32_t>& cls,
-                    uint32_t W, uint32_t s1, const Tuning& tu, bool lc = false, bool node = false) {
+                    uint32_t W, uint32_t s1, const Tuning& tu, bool lc = false, int enc = kEncBlob,
+                    uint32_t cstride = 8) {
     // interval index containing address a
     auto find = [&](uint64_t a) { return (size_t)(std::upper_bound(bnd.begin(), bnd.end(), a) - bnd.begin()) - 1; };
     struct Job {
@@ -105,7 +112,7 @@ uint32_t build_trie(std::vector<uint32_t>& blob, const std::vector<uint64_t>& bn
                 blob[j.block + e] = kLeaf | cls[k];
                 continue;
             }
-            uint32_t st = std::min<uint32_t>(8, j.shift);
+            uint32_t st = std::min<uint32_t>(cstride, j.shift);
             if (lc && j.shift >= 12) {
                 const size_t inside = (size_t)(std::lower_bound(bnd.begin(), bnd.end(), a + span) - bnd.begin()) - k - 1;
                 if (tu.lc_max_stride >= 18 && j.shift >= 18 && inside >= 8192) st = 18;
@@ -113,9 +120,12 @@ uint32_t build_trie(std::vector<uint32_t>& blob, const std::vector<uint64_t>& bn
                 else if (inside >= tu.lc_dense12) st = 12;
             }
             uint32_t child = (uint32_t)blob.size();
-            if ((uint64_t)child + (1ull << st) > (node ? kNodeChildMaxWords : kTrieChildMask)) return kTrieFail;
+            const uint64_t lim = enc == kEncNode ? kNodeChildMaxWords : (enc == kEncWords ? kWordsChildMax : kTrieChildMask);
+            if ((uint64_t)child + (1ull << st) > lim) return kTrieFail;
             blob.resize(blob.size() + (1u << st), 0);
-            blob[j.block + e] = node ? node_entry(child, st, j.shift - st) : child | (st << kTrieStrideShift);
+            blob[j.block + e] = enc == kEncNode    ? node_entry(child, st, j.shift - st)
+                                : enc == kEncWords ? (child << 10 | st << 5 | (j.shift - st))
+                                                   : child | (st << kTrieStrideShift);
             stack.push_back({child, a, j.shift - st, st});
         }
     }
@@ -234,7 +244,7 @@ bool build_fast_table(const DevRule* rules, uint32_t n, uint32_t rule_base, uint
     blob[10] = nsc;
 
     // ---- key classes and the cross product, if it fits ---------------------------------------
-    bool cross = n <= 16384 && tu.pair != 2;  // pair = 2: PAIR wherever it fits (tests)
+    bool cross = n <= tu.cross_max_rules && tu.pair != 2;  // pair = 2: PAIR wherever it fits (tests)
     std::vector<uint64_t> kb{0};
     std::vector<uint32_t> kseg_cls;
     std::vector<std::vector<uint32_t>> key_sets;  // sorted rule indices covering the segment
@@ -242,7 +252,9 @@ bool build_fast_table(const DevRule* rules, uint32_t n, uint32_t rule_base, uint
     std::vector<std::vector<uint32_t>> clist;
     bool lists = false;
     size_t max_list = 0;
-    auto compute_keys = [&]() {
+    // key classes: segments x rules covering them; false when that exceeds the work budget
+    // (e.g. thousands of all-key rules over many segments), then no cross product / PAIR
+    auto compute_keys = [&]() -> bool {
         for (uint32_t i = 0; i < n; i++) {
             if (!live(rules[i])) continue;
             kb.push_back(rules[i].klo);
@@ -261,10 +273,15 @@ bool build_fast_table(const DevRule* rules, uint32_t n, uint32_t rule_base, uint
         std::set<uint32_t> kact;
         std::unordered_map<std::vector<uint32_t>, uint32_t, VecHash> key_cls_of;
         size_t a = 0, b = 0;
+        uint64_t work = 0;
         kseg_cls.resize(kb.size());
         for (size_t k = 0; k < kb.size(); k++) {
             while (b < ke.size() && ke[b].first <= kb[k]) kact.erase(ke[b++].second);
             while (a < ks.size() && ks[a].first <= kb[k]) kact.insert(ks[a++].second);
+            if ((work += kact.size()) > (1ull << 28)) {
+                key_sets.clear();
+                return false;
+            }
             std::vector<uint32_t> v(kact.begin(), kact.end());
             auto it = key_cls_of.find(v);
             if (it == key_cls_of.end()) {
@@ -273,9 +290,12 @@ bool build_fast_table(const DevRule* rules, uint32_t n, uint32_t rule_base, uint
             }
             kseg_cls[k] = it->second;
         }
+        return true;
     };
+    bool keys_ok = true;
     if (cross) {
-        compute_keys();
+        keys_ok = compute_keys();
+        if (!keys_ok) cross = false;
         if ((uint64_t)nsc * key_sets.size() > cross_budget) cross = false;
     }
     if (cross) {
@@ -290,7 +310,7 @@ bool build_fast_table(const DevRule* rules, uint32_t n, uint32_t rule_base, uint
         clist.assign((size_t)nsc * nkc, {});
         for (uint32_t s = 0; s < nsc && cross; s++) {
             for (uint32_t c = 0; c < nkc; c++) {
-                const uint64_t* bits = &kbits[(size_t)c * words];
+                const uint64_t* bits = kbits.data() + (size_t)c * words;
                 std::vector<uint32_t>& L = clist[(size_t)s * nkc + c];
                 for (uint32_t r : src_lists[s]) {
                     if (!((bits[r / 64] >> (r % 64)) & 1)) continue;
@@ -322,7 +342,7 @@ bool build_fast_table(const DevRule* rules, uint32_t n, uint32_t rule_base, uint
     // of its ordered rule list (the src list filtered by dst, truncated at the first rule
     // matching every key), and that class times the key class to the first rule covering it.
     auto try_pair = [&]() -> bool {
-        if (key_sets.empty()) compute_keys();
+        if (!keys_ok || (key_sets.empty() && !(keys_ok = compute_keys()))) return false;
         const uint32_t nkc = (uint32_t)key_sets.size();
         // dst elementary intervals, classed by the set of dst-specific rules covering them
         std::vector<uint64_t> db{0};
@@ -372,7 +392,7 @@ bool build_fast_table(const DevRule* rules, uint32_t n, uint32_t rule_base, uint
             std::vector<uint32_t> L;
             for (uint32_t sc = 0; sc < nsc; sc++)
                 for (uint32_t d = 0; d < ndc; d++) {
-                    const uint64_t* bits = &dbits[(size_t)d * words];
+                    const uint64_t* bits = dbits.data() + (size_t)d * words;
                     L.clear();
                     for (uint32_t r : src_lists[sc]) {
                         if (rules[r].dmask != 0 && !((bits[r / 64] >> (r % 64)) & 1)) continue;
@@ -394,7 +414,7 @@ bool build_fast_table(const DevRule* rules, uint32_t n, uint32_t rule_base, uint
                 std::vector<uint32_t> xv((size_t)npc * nkc, dflt);
                 for (uint32_t p = 0; p < npc; p++)
                     for (uint32_t c = 0; c < nkc; c++) {
-                        const uint64_t* bits = &kbits[(size_t)c * words];
+                        const uint64_t* bits = kbits.data() + (size_t)c * words;
                         for (uint32_t r : pc_lists[p])
                             if ((bits[r / 64] >> (r % 64)) & 1) {
                                 xv[(size_t)p * nkc + c] = verdict(r);
@@ -525,21 +545,23 @@ bool build_fast_table(const DevRule* rules, uint32_t n, uint32_t rule_base, uint
 }
 
 // ---- FD blob: the fixed-depth form of a dst-independent CROSS table --------------------------
-// Layout (u32 words; entries hold byte offsets, so a blob is < 4 MiB):
+// Layout (u32 words; trie entries hold WORD offsets, kEncWords, so a blob is < 16 MiB):
 //   [0] kFlagFD  [1] default verdict  [2] src root (16)  [3] s1  [4] key root  [5] k1
-//   [6] depth D (reads per field, root included)  [7] bias = 4 - 4 * KLEAF  [8] n_key_classes
-//   [10] n_src_classes
-//   src trie | key trie (node encoding, blobwalk.hpp node_entry; leaves: pointers to self words)
-//   rows: per src class c, {self word, verdict[c][0 .. nkc-1]}
-//   KLEAF: per key class k, a self word
-// A self word at byte A holds A << 10 (stride 0: reading "its child" reads itself), so every
-// lookup is exactly D reads per field plus one verdict read at
-//   (src self) + 4 + 4 * key class = (src self) + (key self) + bias,
-// with no per-lane branch (fd_walk). Only tables without dst lists qualify: their verdict never
-// depends on the dst address, so the kernel does not read the dst stream for them.
+//   [6] depth D (reads per field, root included)  [7] bias = 1 - KSELF  [8] n_key_classes
+//   [9] stage words (the prefix below)  [10] n_src_classes
+//   prefix: header | src root block | key trie (all levels) | KSELF: one self word per key class
+//   then:   src trie levels below the root | rows: per src class c {self word, verdict[c][0..nkc-1]}
+// A self word at word A holds A << 10 (stride 0: reading "its child" reads itself). Trie leaves
+// point at self words: src -> its class's row head, key -> its class's self word. Every lookup
+// is exactly D reads per field plus one verdict read at
+//   (src self) + 1 + key class = (src self) + (key self) + bias,
+// with no per-lane branch (fd_walk). The prefix -- everything a key lookup and the src root
+// read touch -- is what a launch stages in LDS when the whole blob does not fit (device.hip
+// STAGE 5). Only tables no rule of which tests dst qualify (engine.cpp): the kernel then does
+// not read the dst stream.
 namespace {
-// depth (reads, root included) of a node-encoded trie rooted at word `root` with 2^s1 entries
-uint32_t node_trie_depth(const std::vector<uint32_t>& b, uint32_t root, uint32_t s1) {
+// depth (reads, root included) of a kEncWords trie rooted at word `root` with 2^s1 entries
+uint32_t words_trie_depth(const std::vector<uint32_t>& b, uint32_t root, uint32_t s1) {
     uint32_t d = 1;
     struct J {
         uint32_t at, n, depth;
@@ -552,63 +574,88 @@ uint32_t node_trie_depth(const std::vector<uint32_t>& b, uint32_t root, uint32_t
         for (uint32_t e = 0; e < j.n; e++) {
             const uint32_t v = b[j.at + e];
             if (v & kLeaf) continue;
-            st.push_back({(v >> 10) / 4u, 1u << ((v >> 5) & 31u), j.depth + 1});
+            st.push_back({v >> 10, 1u << ((v >> 5) & 31u), j.depth + 1});
         }
     }
     return d;
 }
-// leaves (kLeaf | class) of a node-encoded trie -> self-word pointers (word of class c: base + c * step)
-void fd_point_leaves(std::vector<uint32_t>& b, uint32_t root, uint32_t s1, uint32_t base, uint32_t step) {
+// entries of a kEncWords trie: leaves (kLeaf | class) -> self-word pointers (class c: base +
+// c * step), child offsets at or above `from` moved by `delta`
+void fd_fix_trie(std::vector<uint32_t>& b, uint32_t root, uint32_t s1, uint32_t base, uint32_t step, uint32_t from,
+                 uint32_t delta) {
     std::vector<std::pair<uint32_t, uint32_t>> st{{root, 1u << s1}};
     while (!st.empty()) {
         auto j = st.back();
         st.pop_back();
         for (uint32_t e = 0; e < j.second; e++) {
             uint32_t& v = b[j.first + e];
-            if (v & kLeaf) v = ((base + (v & ~kLeaf) * step) * 4u) << 10;
-            else st.push_back({(v >> 10) / 4u, 1u << ((v >> 5) & 31u)});
+            if (v & kLeaf) {
+                v = (base + (v & ~kLeaf) * step) << 10;
+                continue;
+            }
+            const uint32_t child = v >> 10;
+            st.push_back({child, 1u << ((v >> 5) & 31u)});  // still at its pre-move offset
+            if (child >= from) v += delta << 10;
         }
     }
 }
 }  // namespace
 
 bool build_fd_blob(const TableAnalysis& A, uint32_t dflt, const Tuning& tu, std::vector<uint32_t>& blob,
-                   uint32_t max_words) {
+                   uint32_t max_words, uint32_t lds_words) {
     if (!A.clist.empty() || A.nsc == 0 || A.nkc == 0) return false;  // dst lists: the verdict reads dst
-    for (bool lc : {true, false}) {
-        blob.assign(16, 0);
-        const uint32_t s1 = std::min<uint32_t>(pick_stride(A.sb.size(), 32, tu), 12u);
-        if (build_trie(blob, A.sb, A.sint_cls, 32, s1, tu, lc, true) != kSrcRoot) continue;
-        const uint32_t k1 = std::min<uint32_t>(pick_stride(A.kb.size(), 18, tu), 12u);
-        const uint32_t kroot = build_trie(blob, A.kb, A.kseg_cls, 18, k1, tu, lc, true);
-        if (kroot == kTrieFail) continue;
-        const uint32_t depth = std::max(node_trie_depth(blob, kSrcRoot, s1), node_trie_depth(blob, kroot, k1));
-        const uint32_t row0 = (uint32_t)blob.size(), rstep = A.nkc + 1;
-        const uint32_t kleaf = row0 + A.nsc * rstep;
-        const uint64_t words = (uint64_t)kleaf + A.nkc;
-        if (words > max_words || words * 4 >= (1u << 22)) continue;
-        fd_point_leaves(blob, kSrcRoot, s1, row0, rstep);
-        fd_point_leaves(blob, kroot, k1, kleaf, 1);
-        blob.resize(words, 0);
+    // trie shapes, fewest levels first: the first whose blob fits LDS (lds_words) is taken;
+    // if none does, the first that fits max_words (read from HBM, its prefix staged)
+    struct Shape {
+        bool lc;
+        uint32_t s1max, cstride;
+    };
+    const Shape shapes[] = {{true, 12, 8}, {false, 12, 8}, {false, 10, 6}, {false, 8, 4}};
+    std::vector<uint32_t> best;
+    for (const Shape& sh : shapes) {
+        const bool lc = sh.lc;
+        const uint32_t s1 = std::min<uint32_t>(pick_stride(A.sb.size(), 32, tu), sh.s1max);
+        const uint32_t k1 = std::min<uint32_t>(pick_stride(A.kb.size(), 18, tu), sh.s1max);
+        const uint32_t P = kSrcRoot + (1u << s1);  // end of the src root block
+        std::vector<uint32_t> st(kSrcRoot, 0), kt(P, 0);
+        if (build_trie(st, A.sb, A.sint_cls, 32, s1, tu, lc, kEncWords, sh.cstride) != kSrcRoot) continue;
+        if (build_trie(kt, A.kb, A.kseg_cls, 18, k1, tu, lc, kEncWords, sh.cstride) != P) continue;
+        const uint32_t ds = words_trie_depth(st, kSrcRoot, s1), dk = words_trie_depth(kt, P, k1);
+        const uint32_t kself = (uint32_t)kt.size();
+        const uint32_t K = kself + A.nkc - P;  // key region: trie + self words
+        const uint32_t below = (uint32_t)st.size() - P;  // src levels below the root
+        const uint32_t row0 = P + K + below, rstep = A.nkc + 1;
+        const uint64_t words = (uint64_t)row0 + (uint64_t)A.nsc * rstep;
+        if (words > max_words || words >= kWordsChildMax) continue;
+        fd_fix_trie(st, kSrcRoot, s1, row0, rstep, P, K);  // src children move up by K
+        fd_fix_trie(kt, P, k1, kself, 1, 0, 0);
+        blob.assign(words, 0);
+        std::copy(st.begin(), st.begin() + P, blob.begin());
+        std::copy(kt.begin() + P, kt.end(), blob.begin() + P);
+        for (uint32_t k = 0; k < A.nkc; k++) blob[kself + k] = (kself + k) << 10;
+        std::copy(st.begin() + P, st.end(), blob.begin() + P + K);
         for (uint32_t c = 0; c < A.nsc; c++) {
             const uint32_t r = row0 + c * rstep;
-            blob[r] = (r * 4u) << 10;
+            blob[r] = r << 10;
             for (uint32_t k = 0; k < A.nkc; k++) blob[r + 1 + k] = A.cverd[(size_t)c * A.nkc + k];
         }
-        for (uint32_t k = 0; k < A.nkc; k++) blob[kleaf + k] = ((kleaf + k) * 4u) << 10;
         blob[0] = kFlagFD;
         blob[1] = dflt;
         blob[2] = kSrcRoot;
         blob[3] = s1;
-        blob[4] = kroot;
+        blob[4] = P;
         blob[5] = k1;
-        blob[6] = depth;
-        blob[7] = 4u - 4u * kleaf;
+        blob[6] = std::max(ds, dk);
+        blob[7] = 1u - kself;
         blob[8] = A.nkc;
+        blob[9] = (P + K + 3u) & ~3u;
         blob[10] = A.nsc;
-        return true;
+        if (blob.size() <= lds_words) return true;
+        if (best.empty()) best.swap(blob);
     }
-    return false;
+    if (best.empty()) return false;
+    blob.swap(best);
+    return true;
 }
 
 // ---- node classifier -------------------------------------------------------------------------
@@ -754,9 +801,9 @@ bool build_node(HostTableSet& h, const std::vector<TableAnalysis*>& an, const st
     std::vector<uint32_t>& img = h.node_img;
     DevNode& N = h.node;
     N.ip_s1 = std::min(pick_stride(gb.size(), 32, tu), tu.node_root_bits);
-    if (build_trie(img, gb, gcls, 32, N.ip_s1, tu, tu.lc_node != 0, true) != 0) return false;
+    if (build_trie(img, gb, gcls, 32, N.ip_s1, tu, tu.lc_node != 0, kEncNode) != 0) return false;
     N.key_k1 = std::min(pick_stride(kb.size(), 18, tu), tu.node_root_bits);
-    N.key_root = build_trie(img, kb, kcls, 18, N.key_k1, tu, false, true);
+    N.key_root = build_trie(img, kb, kcls, 18, N.key_k1, tu, false, kEncNode);
     if (N.key_root == kTrieFail) return false;
     while (img.size() % 2) img.push_back(0);
     N.ipinfo = (uint32_t)img.size();

@@ -146,6 +146,38 @@ bool ContivRuleTable::insert_rule(const ContivRule& r) {
     return true;
 }
 
+void ContivRuleTable::insert_rules(const std::vector<ContivRule>& rs) {
+    if (rs.size() < 64) {
+        for (const ContivRule& r : rs) insert_rule(r);
+        return;
+    }
+    // sorted, first of each equal run kept (a later equal rule is "already in"), then merged
+    // with the table, skipping rules already there
+    std::vector<ContivRule> add(rs);
+    std::stable_sort(add.begin(), add.end(), [](const ContivRule& a, const ContivRule& b) { return a.compare(b) < 0; });
+    add.erase(std::unique(add.begin(), add.end(), [](const ContivRule& a, const ContivRule& b) { return a.compare(b) == 0; }),
+              add.end());
+    std::vector<ContivRule> out;
+    out.reserve(rules.size() + add.size());
+    size_t i = 0, j = 0;
+    while (i < rules.size() || j < add.size()) {
+        if (j == add.size()) {
+            out.push_back(rules[i++]);
+            continue;
+        }
+        if (i == rules.size()) {
+            out.push_back(add[j++]);
+            continue;
+        }
+        const int c = rules[i].compare(add[j]);
+        if (c < 0) out.push_back(rules[i++]);
+        else if (c > 0) out.push_back(add[j++]);
+        else out.push_back(rules[i++]), j++;  // already in the table
+    }
+    rules.swap(out);
+    slice_len = std::max(slice_len, rules.size());  // append(nil) once NumOfRules reached len(Rules)
+}
+
 bool ContivRuleTable::has_rule(const ContivRule& r) const {
     bool present;
     index_of(r, &present);
@@ -488,7 +520,7 @@ TablePtr RendererCacheTxn::build_local_table(const PodID& pod, const PodConfig& 
     t->pods.insert(pod);
     if (cfg.removed) return t;
     const auto& rules = cache->orientation == kEgressOrientation ? cfg.egress : cfg.ingress;
-    for (auto& r : rules) t->insert_rule(r);
+    t->insert_rules(rules);
     for (auto& sp : all_pods()) install_local_rules(*t, cfg, *pod_config(sp));
     if (t->slice_len > 0) {  // len(table.Rules) > 0 (cache_impl.go:496)
         bool all_matched = false;
@@ -559,11 +591,12 @@ void RendererCacheTxn::rebuild_global() {
     bool eg = cache->orientation == kEgressOrientation;
     for (auto& pod : all_pods()) {
         auto cfg = pod_config(pod);
-        for (auto r : (eg ? cfg->ingress : cfg->egress)) {
+        std::vector<ContivRule> rs = eg ? cfg->ingress : cfg->egress;
+        for (auto& r : rs) {
             if (eg) r.src = cfg->pod_ip;
             else r.dst = cfg->pod_ip;
-            global->insert_rule(r);
         }
+        global->insert_rules(rs);
     }
     if (global->num_rules() > 0) global->insert_rule(allow_all_rule());
 }

@@ -81,6 +81,9 @@ struct ContivRuleTable {
     size_t num_rules() const { return rules.size(); }
     const std::string& get_id() const;
     bool insert_rule(const ContivRule& r);
+    // InsertRule of every rule of rs in order, in O((n + k) log k): the same table and
+    // NumOfRules / len(Rules) as k single inserts
+    void insert_rules(const std::vector<ContivRule>& rs);
     bool has_rule(const ContivRule& r) const;
     size_t index_of(const ContivRule& r, bool* present) const;
     template <class P>

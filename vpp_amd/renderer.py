@@ -270,7 +270,8 @@ class Engine:
         f, nbytes, nsc, nkc = (x.value for x in v)
         mode = "linear" if f & 8 else ("fd" if f & 32 else ("pair" if f & 16 else ("cand" if f & 4 else (
             "cross+lists" if f & 2 else "cross"))))
-        return {"structure": mode, "blob_bytes": nbytes, "src_classes": nsc, "key_classes": nkc}
+        return {"structure": mode, "blob_bytes": nbytes, "src_classes": nsc, "key_classes": nkc,
+                "dst_free": bool(f & 64)}
 
     def debug_walk(self, acl_name, src, dst, dport, proto):
         """TESTS ONLY: host walk of the ACL's compiled blob (see pg_debug_walk_blob)."""

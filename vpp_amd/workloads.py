@@ -12,6 +12,9 @@ this path); shapes follow the reference's own fixtures and perf generator:
   config 4  100k-rule ACL ingested directly (vpp_acl key space), disjoint src prefixes,
             first-match depth Zipf(1.1), 5 % no-match
   config 5  config-3 topology in connection mode with per-rule hit counters
+  config 7  the whole tests/policy/perf/gen-policy.py policy (1000 CIDRs x 5 excepts x 20 ports,
+            ingress and egress) through the policy configurator: the pod's ~487k-rule table
+  rule-count sweep: config 2's shape at any rule count (bench.py --rules N)
 """
 import random
 
@@ -20,7 +23,7 @@ import numpy as np
 from . import renderer as R
 from ._capi import MODE_CONN, MODE_PERPOD, MODE_SINGLE
 
-SEEDS = {1: 0xC0DE0001, 2: 0xC0DE0002, 3: 0xC0DE0003, 4: 0xC0DE0004, 5: 0xC0DE0005, 6: 0xC0DE0006}
+SEEDS = {1: 0xC0DE0001, 2: 0xC0DE0002, 3: 0xC0DE0003, 4: 0xC0DE0004, 5: 0xC0DE0005, 6: 0xC0DE0006, 7: 0xC0DE0007}
 POPULAR_PORTS = [22, 53, 67, 80, 81, 161, 162, 443, 514, 8080]
 
 
@@ -142,13 +145,15 @@ def gen_policy_rules(seed, max_rules=999, num_excepts=5, num_ports=20):
     return rules[:max_rules]
 
 
-def config2(device=0, n_tuples=64 << 20):
+def config2(device=0, n_tuples=64 << 20, n_rules=1000):
+    """n_rules: the table's rules (n_rules - 1 generated + deny-the-rest); 1000 = BASELINE's config 2"""
     e = _new_engine(device)
     pod = "default/db-0"
     e.SetPodIfName(pod, "node1-tap-db0")
     e.RegisterPod(pod, "10.1.0.10", False)
     r = R.Renderer(e)
-    rules = gen_policy_rules(SEEDS[2]) + [R.ContivRule(R.ActionDeny, R.IPNet(), R.IPNet(), R.ANY, 0, 0)]
+    rules = gen_policy_rules(SEEDS[2], max_rules=n_rules - 1) + [R.ContivRule(R.ActionDeny, R.IPNet(), R.IPNet(), R.ANY,
+                                                                              0, 0)]
     t = r.NewTxn(True)
     t.Render(pod, R.IPNet.host("10.1.0.10"), [], rules, False)
     err = t.Commit()
@@ -158,6 +163,63 @@ def config2(device=0, n_tuples=64 << 20):
     gen = dict(seed=SEEDS[2], table_id=tid, inside_pct=50, tcp_pct=45, udp_pct=45)
     return Workload(2, e, MODE_SINGLE, tid, gen, n_tuples, "gen-policy 1k-rule table (%d rules)" % len(acl["rules"]),
                     r)
+
+
+def gen_policy_blocks(rnd, num_cidrs=1000, num_excepts=5):
+    """tests/policy/perf/gen-policy.py:39-51 genIpBlocks: CIDR i under (i + 0x100) << 16, mask
+    /16-/24, five /24-/32 excepts inside it"""
+    from . import configurator as CF
+    blocks = []
+    for i in range(num_cidrs):
+        prefix = (i + 0x100) << 16
+        cidr = rnd.randint(prefix, prefix | 0xFFFF)
+        ml = rnd.randint(16, 24)
+        cidr = mask_ip(cidr, ml)
+        ex = []
+        for _ in range(num_excepts):
+            e = rnd.randint(cidr, cidr | ((1 << (32 - ml)) - 1))
+            el = rnd.randint(24, 32)
+            ex.append("%s/%d" % (ip_str(mask_ip(e, el)), el))
+        blocks.append(CF.IPBlock("%s/%d" % (ip_str(cidr), ml), ex))
+    return blocks
+
+
+def gen_policy_ports(rnd, num_ports=20):
+    """gen-policy.py:53-62 genPorts"""
+    from . import configurator as CF
+    return [CF.Port(CF.TCP if rnd.randint(0, 1) == 0 else CF.UDP, rnd.randint(0, 65535)) for _ in range(num_ports)]
+
+
+def config7(device=0, n_tuples=64 << 20):
+    """The whole gen-policy.py NetworkPolicy (1000 ingress + 1000 egress ipBlocks with 5 excepts
+    each, 20 ports each) for pod role=db, through the policy configurator (IPBlock minus excepts
+    by subtractSubnet, x ports, NAT-loopback permit, deny-the-rest) into the GPU renderer; SINGLE
+    mode on the pod's table (the ingress part, ~487k rules; the egress part lands in the
+    global table)."""
+    from . import configurator as CF
+    e = _new_engine(device)
+    pod, ip = "default/db-0", "10.1.0.10"
+    e.SetPodIfName(pod, "node1-tap-db0")
+    e.RegisterPod(pod, ip, False)
+    r = R.Renderer(e)
+    rnd = random.Random(SEEDS[7])
+    ing = CF.Match(CF.MatchIngress, IPBlocks=gen_policy_blocks(rnd), Ports=gen_policy_ports(rnd))
+    eg = CF.Match(CF.MatchEgress, IPBlocks=gen_policy_blocks(rnd), Ports=gen_policy_ports(rnd))
+    cfg = CF.PolicyConfigurator()
+    cfg.AddPodConfig(pod, ip)
+    cfg.SetNatLoopbackIP(NAT_LOOPBACK_IP)
+    assert cfg.RegisterRenderer(r) is None
+    t = cfg.NewTxn(True)
+    t.Configure(pod, [CF.ContivPolicy("default/test-network-policy", CF.PolicyAll, [ing, eg])])
+    err = t.Commit()
+    assert err is None, err
+    acl = e.GetOutboundACL("node1-tap-db0")
+    tid = e.table_id(acl["name"])
+    gen = dict(seed=SEEDS[7], table_id=tid, inside_pct=50, tcp_pct=45, udp_pct=45)
+    w = Workload(7, e, MODE_SINGLE, tid, gen, n_tuples,
+                 "gen-policy.py policy through the configurator (%d-rule pod table)" % len(acl["rules"]), r)
+    w.control = cfg
+    return w
 
 
 # ---- config 4 ------------------------------------------------------------------------
@@ -459,4 +521,4 @@ def table_histogram(e):
     return dict(sorted(h.items()))
 
 
-CONFIGS = {1: config1, 2: config2, 3: config3, 4: config4, 5: config5, 6: config6}
+CONFIGS = {1: config1, 2: config2, 3: config3, 4: config4, 5: config5, 6: config6, 7: config7}
