@@ -197,3 +197,43 @@ def test_common_rows_disabled():
         assert np.array_equal(e2.debug_classify_host(MODE_CONN, -1, *tup, node=True), on)
     finally:
         assert _capi.lib.pg_set_tuning(b"node_common", 1) == 0
+
+
+def _pair_coverage(e):
+    """(tables in PAIR form, of them covered by the node): tabinfo words are internal, so read
+    the coverage through the node's behaviour: a covered PAIR table classifies through the node
+    exactly like through its per-table blob, which check() asserts; here only the structures."""
+    return [e.table_stats(t)["structure"] for t in range(e.num_tables())].count("pair")
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_pair_tables_in_the_node(seed):
+    """Tables in the PAIR form (src class x dst class -> pair class x key class; forced with
+    pair = 2 on dst-specific random ACLs) are covered by the node classifier: node == per-table
+    == oracle, PERPOD and CONN, with counters, weird rules included."""
+    e0 = R.Engine(0)
+    try:
+        assert _capi.lib.pg_set_tuning(b"pair", 2) == 0
+        rnd = random.Random(3000 + seed)
+        e, local, pod_ips = topology(rnd, weird=seed % 2 == 1)
+    finally:
+        assert _capi.lib.pg_set_tuning(b"pair", 1) == 0
+    assert e0.get_tuning("pair") == 1 and e.get_tuning("pair") == 2
+    assert _pair_coverage(e) >= 3
+    check(e, local, tuples(seed, 30011, pod_ips))
+
+
+def test_config6_pair_table_covered():
+    """config 6's 36.5k-rule global table (PAIR) is in the node: its image grows by the table's
+    class map and PERPOD equals the per-table path and the oracle on a sample."""
+    w = W.config6(0, n_tuples=1 << 10)
+    e = w.engine
+    big = [t for t in range(e.num_tables()) if e.table_info(t)[1] > 30000]
+    assert big and e.table_stats(big[0])["structure"] == "pair"
+    ns = e.node_stats()
+    assert ns is not None and ns["image_bytes"] <= 64 << 10, ns
+    src, dst, sport, dport, proto = gen.gen_tuples(40000, **w.gen)
+    wd = World(e, w.local_ifs, w.node_if)
+    act, slot = wd.perpod(src, dst, dport, proto, threads=8)
+    got = e.debug_classify_host(MODE_PERPOD, -1, src, dst, sport, dport, proto, node=True)
+    assert np.array_equal(got >> 30, act.astype(np.uint32)) and np.array_equal(got & 0x3FFFFFFF, slot)

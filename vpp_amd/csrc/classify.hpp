@@ -27,9 +27,6 @@ namespace pg {
 #ifndef PG_AGG_ROUNDS  // wave-aggregation rounds of hit-counter increments (Hist::inc)
 #define PG_AGG_ROUNDS 0
 #endif
-#ifndef PG_NODE_BF  // node evaluations: table-info reads without per-tuple branches
-#define PG_NODE_BF 1
-#endif
 #ifndef PG_NODE_FB_Q1  // node kernels: per-table fallback one tuple at a time
 #define PG_NODE_FB_Q1 1
 #endif
@@ -405,11 +402,11 @@ struct NodeEval {
                      uint32_t (&w)[Q]) const {
         const DevLoader X{N.cross};
         const uint32_t(&k)[Q] = rev ? kack : ksyn;
-        const uint32_t(&ca)[Q] = rev ? cd : cs;
+        const uint32_t(&ca)[Q] = rev ? cd : cs;  // the IP class on the rule's src side
+        const uint32_t(&cb)[Q] = rev ? cs : cd;  // ... and on its dst side (PAIR tables)
         const uint32_t(&gk)[Q] = rev ? gack : gsyn;
-        bool cm[Q];
-        uint32_t pos[Q];
-#if PG_NODE_BF
+        bool cm[Q], pr[Q];
+        uint32_t pos[Q], pv[Q] = {}, pk[Q] = {};
         // branch-free: every lane reads its (or table 0's) image words, the flags select
         PG_UNROLL
         for (int j = 0; j < Q; j++) {
@@ -426,31 +423,16 @@ struct NodeEval {
             cm[j] = CM && (cw & 1u);
             pos[j] = cm[j] ? ti.z + lk : ti.x + ca[j] * (ti.y & 0xFFFFu) + lk;
             fb[j] = act[j] && !on[j];
-        }
-#else
-        PG_UNROLL
-        for (int j = 0; j < Q; j++) {
-            on[j] = cm[j] = false;
-            pos[j] = 0;
-            if (act[j] && k[j] < kWalkKeyLimit) {
-                // {cross base, nkc | covered << 31, common row, 0}
-                const W4 ti = img.u4(N.tabinfo + 4u * (uint32_t)t[j]);
-                if (ti.y >> 31) {
-                    const uint32_t ki = (uint32_t)t[j] * N.gk + gk[j];
-                    uint32_t cw = 0;
-                    if (CM) {
-                        const uint32_t b = (uint32_t)t[j] * N.n_ipc + ca[j];
-                        cw = img.u32(N.cmap + (b >> 5u)) >> (b & 31u);
-                    }
-                    const uint32_t lk = (img.u32(N.kmap + (ki >> 1)) >> ((ki & 1u) * 16u)) & 0xFFFFu;
-                    cm[j] = CM && (cw & 1u);
-                    pos[j] = cm[j] ? ti.z + lk : ti.x + ca[j] * (ti.y & 0xFFFFu) + lk;
-                    on[j] = true;
-                }
+            // PAIR table (kNodePairFlag): the pair map entry first, its verdict row after
+            pr[j] = on[j] && (ti.y & kNodePairFlag);
+            if (pr[j]) {
+                const uint32_t mo = ti.w & 0xFFFFu;
+                const uint32_t sc = img.u32(mo + ca[j]) & 0xFFFFu, dc = img.u32(mo + cb[j]) >> 16;
+                pos[j] = ti.x + sc * (ti.w >> 16) + dc;
+                pv[j] = ti.z + lk;
+                pk[j] = ti.y & 0xFFFFu;
             }
-            fb[j] = act[j] && !on[j];
         }
-#endif
         PG_UNROLL
         for (int j = 0; j < Q; j++) {
             if (!on[j]) continue;
@@ -460,6 +442,9 @@ struct NodeEval {
             if (!cm[j]) w[j] = X.u32(pos[j]);
 #endif
         }
+        PG_UNROLL
+        for (int j = 0; j < Q; j++)
+            if (pr[j]) w[j] = X.u32(pv[j] + w[j] * pk[j]);
         if (CM) {
             PG_UNROLL
             for (int j = 0; j < Q; j++)

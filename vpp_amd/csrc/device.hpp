@@ -53,8 +53,15 @@ struct DevTable {          // 32 B: two 16-B loads
 //                 bit set = that (table, ip class) row equals the table's common row, so the
 //                 entry is read from the (LDS-staged) image instead of the cross table
 //   cross  u32[]  per covered table, [ip class][local key class] -> verdict, or kNodeList |
-//                 first dst record (16 B records, blobwalk.hpp, ending with a match-all one)
+//                 first dst record (16 B records, blobwalk.hpp, ending with a match-all one);
+//                 per covered PAIR table its pair map [src class][dst class] -> pair class and
+//                 its verdicts [pair class][local key class] (the image then holds, per node IP
+//                 class, the table's src class | dst class << 16)
 constexpr uint32_t kNodeList = 1u << 29, kNodeRecMask = kNodeList - 1u;
+// tabinfo.y bit 30: a PAIR table (tabinfo = {pair map base, nkc | covered << 31 | 1 << 30,
+// verdicts base, class map offset | ndc << 16}): (src class of the src-side IP class, dst class of
+// the dst-side one) -> pair class by one cross-array entry, then x local key class -> verdict
+constexpr uint32_t kNodePairFlag = 1u << 30;
 struct DevNode {
     const uint32_t* img;   // null: no node classifier (the per-table path runs)
     const uint32_t* cross;

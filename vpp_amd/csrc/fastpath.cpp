@@ -162,6 +162,13 @@ struct TableAnalysis {
     uint32_t nkc = 0;
     std::vector<uint32_t> cverd;       // [src class][key class] verdict
     std::vector<std::vector<uint32_t>> clist;  // dst-specific rules in front of it
+    // PAIR tables (cverd / clist empty): dst intervals and classes, the (src class, dst
+    // class) -> pair class map and the pair class x key class verdicts
+    bool pair = false;
+    std::vector<uint64_t> db;
+    std::vector<uint32_t> dint_cls;
+    uint32_t ndc = 0, npc = 0;
+    std::vector<uint32_t> pmap, xv;
 };
 
 void free_analysis(TableAnalysis* an) { delete an; }
@@ -447,6 +454,25 @@ bool build_fast_table(const DevRule* rules, uint32_t n, uint32_t rule_base, uint
                 blob[13] = d1;
                 blob[14] = (uint32_t)poff;
                 blob[15] = ndc;
+                if (an) {  // the node classifier covers PAIR tables too (build_node)
+                    auto* a = new TableAnalysis();
+                    a->rules = rules;
+                    a->rule_base = rule_base;
+                    a->sb = sb;
+                    a->sint_cls = sint_cls;
+                    a->nsc = nsc;
+                    a->kb = kb;
+                    a->kseg_cls = kseg_cls;
+                    a->nkc = nkc;
+                    a->pair = true;
+                    a->db = db;
+                    a->dint_cls = dint_cls;
+                    a->ndc = ndc;
+                    a->npc = npc;
+                    a->pmap.swap(pmap);
+                    a->xv.swap(xv);
+                    *an = a;
+                }
                 return true;
             }
         }
@@ -603,7 +629,7 @@ void fd_fix_trie(std::vector<uint32_t>& b, uint32_t root, uint32_t s1, uint32_t 
 
 bool build_fd_blob(const TableAnalysis& A, uint32_t dflt, const Tuning& tu, std::vector<uint32_t>& blob,
                    uint32_t max_words, uint32_t lds_words) {
-    if (!A.clist.empty() || A.nsc == 0 || A.nkc == 0) return false;  // dst lists: the verdict reads dst
+    if (A.pair || !A.clist.empty() || A.nsc == 0 || A.nkc == 0) return false;  // dst lists: the verdict reads dst
     // trie shapes, fewest levels first: the first whose blob fits LDS (lds_words) is taken;
     // if none does, the first that fits max_words (read from HBM, its prefix staged)
     struct Shape {
@@ -726,12 +752,18 @@ bool build_node(HostTableSet& h, const std::vector<TableAnalysis*>& an, const st
     if (!tu.node_build || T == 0 || T >= 0xFFFFu) return false;
     std::vector<uint32_t> cov;
     for (uint32_t t = 0; t < T; t++)
-        if (an[t] && an[t]->nkc <= 0xFFFFu) cov.push_back(t);
+        if (an[t] && an[t]->nkc <= 0xFFFFu && (!an[t]->pair || (an[t]->nsc <= 0xFFFFu && an[t]->ndc <= 0xFFFFu)))
+            cov.push_back(t);
     if (cov.empty()) return false;
+    // PAIR tables among them: the IPv4 partition also separates their dst classes
+    std::vector<size_t> pcov;  // indices into cov
+    for (size_t c = 0; c < cov.size(); c++)
+        if (an[cov[c]]->pair) pcov.push_back(c);
 
     // IPv4 partition
     std::vector<uint64_t> gb{0};
     for (uint32_t t : cov) gb.insert(gb.end(), an[t]->sb.begin(), an[t]->sb.end());
+    for (size_t c : pcov) gb.insert(gb.end(), an[cov[c]]->db.begin(), an[cov[c]]->db.end());
     if ((uint64_t)h.rules.size() + T + 2 >= kNodeList) return false;  // verdict slots below the list flag
     std::map<uint32_t, NodePod> by_ip;  // a repeated address: the last pod wins, as in the iphash
     for (const NodePod& p : pods) by_ip[p.ip] = p;
@@ -744,12 +776,14 @@ bool build_node(HostTableSet& h, const std::vector<TableAnalysis*>& an, const st
     std::sort(gb.begin(), gb.end());
     gb.erase(std::unique(gb.begin(), gb.end()), gb.end());
     const size_t C = cov.size();
-    std::vector<size_t> at(C, 0);
+    const size_t PC = pcov.size();
+    std::vector<size_t> at(C, 0), atd(PC, 0);
     std::unordered_map<std::vector<uint32_t>, uint32_t, VecHash> ipc_of;
-    std::vector<std::vector<uint32_t>> ipc_key;  // class -> {ifc, tin, tout, local src classes...}
+    // class -> {ifc, tin, tout, src class per covered table..., dst class per PAIR table...}
+    std::vector<std::vector<uint32_t>> ipc_key;
     std::vector<uint32_t> gcls(gb.size());
     size_t pi = 0;
-    std::vector<uint32_t> key(3 + C);
+    std::vector<uint32_t> key(3 + C + PC);
     for (size_t k = 0; k < gb.size(); k++) {
         const uint64_t a = gb[k];
         while (pi < ps.size() && ps[pi].ip < a) pi++;
@@ -760,6 +794,11 @@ bool build_node(HostTableSet& h, const std::vector<TableAnalysis*>& an, const st
             while (at[c] + 1 < A.sb.size() && A.sb[at[c] + 1] <= a) at[c]++;
             key[3 + c] = A.sint_cls[at[c]];
         }
+        for (size_t q = 0; q < PC; q++) {
+            const TableAnalysis& A = *an[cov[pcov[q]]];
+            while (atd[q] + 1 < A.db.size() && A.db[atd[q] + 1] <= a) atd[q]++;
+            key[3 + C + q] = A.dint_cls[atd[q]];
+        }
         auto it = ipc_of.find(key);
         if (it == ipc_of.end()) {
             it = ipc_of.emplace(key, (uint32_t)ipc_key.size()).first;
@@ -769,7 +808,9 @@ bool build_node(HostTableSet& h, const std::vector<TableAnalysis*>& an, const st
     }
     const uint32_t G = (uint32_t)ipc_key.size();
     uint64_t entries = 0;
-    for (uint32_t t : cov) entries += (uint64_t)G * an[t]->nkc;
+    for (uint32_t t : cov)
+        entries += an[t]->pair ? (uint64_t)an[t]->nsc * an[t]->ndc + (uint64_t)an[t]->npc * an[t]->nkc
+                               : (uint64_t)G * an[t]->nkc;
     if (entries > kNodeCrossBudget) return false;
 
     // L4-key partition
@@ -819,6 +860,14 @@ bool build_node(HostTableSet& h, const std::vector<TableAnalysis*>& an, const st
     N.kmap = (uint32_t)img.size();
     img.resize(img.size() + ((size_t)T * GK + 1) / 2, 0);
     while (img.size() % 4) img.push_back(0);
+    // PAIR tables: per node IP class, the table's src class | dst class << 16
+    std::vector<uint32_t> pmap_off(PC);
+    for (size_t q = 0; q < PC; q++) {
+        pmap_off[q] = (uint32_t)img.size();
+        for (uint32_t g = 0; g < G; g++) img.push_back(ipc_key[g][3 + pcov[q]] | (ipc_key[g][3 + C + q] << 16));
+    }
+    while (img.size() % 4) img.push_back(0);
+    if (img.size() >= 0xFFFFu) return false;  // map offsets are 16-bit (tabinfo.w)
     N.gk = GK;
     N.n_ipc = G;
     N.img_words = N.img_words_base = (uint32_t)img.size();
@@ -829,6 +878,7 @@ bool build_node(HostTableSet& h, const std::vector<TableAnalysis*>& an, const st
     X.reserve(entries + 16);
     std::vector<uint32_t> recs;
     const size_t rec0 = (entries + 3) & ~(uint64_t)3;
+    size_t q = 0;
     for (size_t c = 0; c < C; c++) {
         const uint32_t t = cov[c];
         const TableAnalysis& A = *an[t];
@@ -837,6 +887,14 @@ bool build_node(HostTableSet& h, const std::vector<TableAnalysis*>& an, const st
         for (uint32_t g = 0; g < GK; g++) {
             const uint32_t ki = t * GK + g;
             img[N.kmap + ki / 2] |= kc_key[g][c] << ((ki & 1u) * 16u);
+        }
+        if (A.pair) {  // {pair map base, nkc | covered | PAIR, verdicts base, class map | ndc << 16}
+            img[N.tabinfo + 4 * t + 1] |= kNodePairFlag;
+            X.insert(X.end(), A.pmap.begin(), A.pmap.end());
+            img[N.tabinfo + 4 * t + 2] = (uint32_t)X.size();
+            X.insert(X.end(), A.xv.begin(), A.xv.end());
+            img[N.tabinfo + 4 * t + 3] = pmap_off[q++] | (A.ndc << 16);
+            continue;
         }
         std::vector<uint32_t> first(A.clist.empty() ? 0 : A.cverd.size(), 0xFFFFFFFFu);
         for (uint32_t g = 0; g < G; g++) {
@@ -867,7 +925,10 @@ bool build_node(HostTableSet& h, const std::vector<TableAnalysis*>& an, const st
             }
         }
     }
-    build_common_rows(h, cov, an, tu);
+    std::vector<uint32_t> xcov;  // the cross-product tables (common rows); PAIR tables have none
+    for (uint32_t t : cov)
+        if (!an[t]->pair) xcov.push_back(t);
+    build_common_rows(h, xcov, an, tu);
     X.resize(rec0, 0);
     X.insert(X.end(), recs.begin(), recs.end());
     if (X.empty()) X.resize(4, 0);
