@@ -172,6 +172,11 @@ def main():
     }
     if allreduce is not None:
         line.update(allreduce)
+    # the same fraction against what a plain device copy reaches on this GPU (after the timed
+    # region): read + write of a 1 GiB buffer
+    cp, rd = stream_peaks_gbps()
+    line["roofline"]["measured_stream_gbps"] = {"copy": cp, "read": rd}
+    line["roofline"]["frac_of_measured_stream"] = round(achieved / max(cp, rd), 4)
     if rank == 0 and world == 1 and not a.no_cpu:
         line["cpu_baseline"], line["parity_sample"] = cpu_baseline(w, b, out, a.cpu_sample, a.faithful_seconds,
                                                                    a.cpu_seconds)
@@ -258,6 +263,31 @@ def dry_run(a, rank, world):
         dist.destroy_process_group()
 
 
+def stream_peaks_gbps(nbytes=1 << 30, reps=10):
+    """measured HBM stream rates on this GPU (torch's own kernels, median of reps): a
+    device-to-device copy (bytes read + written / time) and a read-only fp32 sum (bytes read /
+    time); the classify kernels read 7-13 B and write 4 B per tuple, between the two"""
+    x = torch.ones(nbytes // 4, dtype=torch.float32, device="cuda")
+    y = torch.empty_like(x)
+
+    def med(fn):
+        fn()
+        ts = []
+        for _ in range(reps):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            fn()
+            e1.record()
+            torch.cuda.synchronize()
+            ts.append(e0.elapsed_time(e1))
+        return sorted(ts)[len(ts) // 2] * 1e-3
+
+    copy = 2 * nbytes / med(lambda: y.copy_(x)) / 1e9
+    read = nbytes / med(lambda: x.sum()) / 1e9
+    del x, y
+    return round(copy, 1), round(read, 1)
+
+
 def bytes_per_tuple(w):
     """Algorithmic bytes per tuple: the tuple fields the classification reads
     plus the 4-B verdict. SINGLE / PERPOD read src 4 + dst 4 + dport 2 + proto 1 = 11 B (15 B
@@ -339,6 +369,11 @@ def cpu_baseline(w, b, out, k, faithful_s=8.0, budget_s=10.0):
         extra["faithful_1thread_mpps"] = round(kf / (time.perf_counter() - t0) / 1e6, 4)
         extra["faithful_sample"] = kf
         fslot = np.where(fi >= 0, base + fi.astype(np.int64), dflt).astype(np.uint32)
+        # rules the reference's first-match loop (aclengine_mock.go:510-649) visits per tuple
+        nr = len(rules)
+        visited = np.where(idx >= 0, idx.astype(np.int64) + 1, nr)
+        extra["reference_rules_visited"] = {"mean": round(float(visited.mean()), 1),
+                                            "p99": int(np.percentile(visited, 99)), "rules": nr}
         faithful_ok = bool(((got[:kf] >> 30) == fa.astype(np.uint32)).all() and ((got[:kf] & 0x3FFFFFFF) == fslot).all())
     else:
         wd = world.World(e, w.local_ifs, w.node_if)

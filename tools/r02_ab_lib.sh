@@ -1,0 +1,32 @@
+#!/bin/bash
+# A/B of two builds (sweep.py in alternating processes) on the given configs, 2 rounds.
+#   gpurun -- bash tools/r02_ab_lib.sh TAG "libA libB" "3 5c 6" [pytest paths]
+set -o pipefail
+TAG=${1:-ablib}; LIBS=${2:-libpolicygpu.so}; CONFIGS=${3:-3}; TESTS=${4:-}
+R=$(pwd)
+O=$R/gpurun_out/$TAG
+mkdir -p "$O"
+step() { echo "[$(date +%T)] $*"; }
+if [ -n "$TESTS" ]; then
+    step tests $TESTS
+    timeout -k 10 800 python -u -m pytest $TESTS -m gpu -x -q --timeout 300 --timeout-method thread \
+        > "$O/gpu_tests.log" 2>&1 || { tail -30 "$O/gpu_tests.log"; exit 1; }
+    tail -2 "$O/gpu_tests.log"
+fi
+for r in 1 2; do
+for lib in $LIBS; do
+    for c in $CONFIGS; do
+        cnt=""; case $c in *c) cnt="--counters";; esac
+        extra=""; case $c in r*) extra="--rules ${c#r}"; c=2;; esac
+        step sweep $lib config $c $cnt $extra
+        VPP_AMD_LIB=$R/vpp_amd/$lib timeout -k 10 200 python tools/sweep.py --config ${c%c} --rounds 3 --reps 5 $cnt \
+            >> "$O/sweep.jsonl" 2> "$O/sweep.err" || { tail -20 "$O/sweep.err"; exit 1; }
+    done
+done
+done
+python -c "
+import json
+for l in open('$O/sweep.jsonl'):
+    d=json.loads(l); print(d['lib'], d['config'], d['counters'], d['ms'], d['gpps'])
+"
+step done

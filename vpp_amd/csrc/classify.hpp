@@ -289,69 +289,53 @@ struct TabEval {
 // table per evaluation, cross[tabinfo[t].base + ipclass * nkc_t + kmap[t][keyclass]]: a
 // verdict, or (kNodeList) the first of the dst records to test. Tables the node does not
 // cover, LINEAR tables and ANY-protocol packets take the per-table path.
-// Q trie lookups in lockstep (root stride s1 over a W-bit address, then each node's stride).
-// PRED: one load per tuple per level, no per-tuple branches (LDS images).
-// Node-image encoding of the non-leaf entries (blobwalk.hpp node_entry).
+// Fixed-depth trie lookups (DevNode: leaves point at their class's self word, which points
+// at itself), in lockstep and without per-lane branches: the root read (stride s1 over a W-bit
+// address), then depth - 1 steps of one bit-field extract and one shifted add each (blobwalk.hpp
+// node_child_byte); the class is the self word's index. PRED is unused (kept for the callers).
 template <bool PRED, class L, int Q>
-PG_HD void node_trie_q(const L& ld, uint32_t root, uint32_t s1, uint32_t W, const uint32_t (&a)[Q], uint32_t (&c)[Q]) {
+PG_HD void node_trie_q(const L& ld, uint32_t root, uint32_t s1, uint32_t W, uint32_t depth, uint32_t self0,
+                       const uint32_t (&a)[Q], uint32_t (&c)[Q]) {
     uint32_t e[Q];
     PG_UNROLL
     for (int j = 0; j < Q; j++) e[j] = ld.u32(root + (a[j] >> (W - s1)));
-    for (;;) {
-        bool more = false;
+    for (uint32_t l = 1; l < depth; l++) {
         PG_UNROLL
-        for (int j = 0; j < Q; j++) more |= !(e[j] & kLeaf);
-        if (!more) break;
-        PG_UNROLL
-        for (int j = 0; j < Q; j++) {
-            if (PRED) {
-                const bool d = !(e[j] & kLeaf);
-                const uint32_t v = ld.at_byte(d ? node_child_byte(e[j], a[j]) : 0u);
-                e[j] = d ? v : e[j];
-                continue;
-            }
-            if (e[j] & kLeaf) continue;
-            e[j] = ld.at_byte(node_child_byte(e[j], a[j]));
-        }
+        for (int j = 0; j < Q; j++) e[j] = ld.at_byte(node_child_byte(e[j], a[j]));
     }
     PG_UNROLL
-    for (int j = 0; j < Q; j++) c[j] = e[j] & ~kLeaf;
+    for (int j = 0; j < Q; j++) c[j] = (e[j] >> 12) - self0;
 }
 
-// Two tries of the node image walked in one lockstep loop (IPv4 addresses a over the root at
-// 0, L4 keys b over the key root): the walks are independent, so their dependent LDS reads
-// overlap instead of running one trie after the other. Below the roots a step needs only the
-// entry and the address (node_child_byte), whichever trie it belongs to.
+// The IPv4 trie (addresses a) and the L4-key trie (keys b) in one lockstep loop: independent
+// walks, so their dependent LDS reads overlap.
 template <bool PRED, class L, int QA, int QB>
 PG_HD void node_trie2_q(const L& ld, const DevNode& N, const uint32_t (&a)[QA], uint32_t (&ca)[QA],
                         const uint32_t (&b)[QB], uint32_t (&cb)[QB]) {
-    constexpr int Q = QA + QB;
-    uint32_t x[Q], e[Q];
+    uint32_t ea[QA], eb[QB];
     PG_UNROLL
-    for (int j = 0; j < QA; j++) x[j] = a[j], e[j] = ld.u32(a[j] >> (32u - N.ip_s1));
+    for (int j = 0; j < QA; j++) ea[j] = ld.u32(a[j] >> (32u - N.ip_s1));
     PG_UNROLL
-    for (int j = 0; j < QB; j++) x[QA + j] = b[j], e[QA + j] = ld.u32(N.key_root + (b[j] >> (18u - N.key_k1)));
-    for (;;) {
-        bool more = false;
+    for (int j = 0; j < QB; j++) eb[j] = ld.u32(N.key_root + (b[j] >> (18u - N.key_k1)));
+    const uint32_t dmin = N.ip_depth < N.key_depth ? N.ip_depth : N.key_depth;
+    for (uint32_t l = 1; l < dmin; l++) {
         PG_UNROLL
-        for (int j = 0; j < Q; j++) more |= !(e[j] & kLeaf);
-        if (!more) break;
+        for (int j = 0; j < QA; j++) ea[j] = ld.at_byte(node_child_byte(ea[j], a[j]));
         PG_UNROLL
-        for (int j = 0; j < Q; j++) {
-            if (PRED) {
-                const bool d = !(e[j] & kLeaf);
-                const uint32_t v = ld.at_byte(d ? node_child_byte(e[j], x[j]) : 0u);
-                e[j] = d ? v : e[j];
-                continue;
-            }
-            if (e[j] & kLeaf) continue;
-            e[j] = ld.at_byte(node_child_byte(e[j], x[j]));
-        }
+        for (int j = 0; j < QB; j++) eb[j] = ld.at_byte(node_child_byte(eb[j], b[j]));
+    }
+    for (uint32_t l = dmin; l < N.ip_depth; l++) {
+        PG_UNROLL
+        for (int j = 0; j < QA; j++) ea[j] = ld.at_byte(node_child_byte(ea[j], a[j]));
+    }
+    for (uint32_t l = dmin; l < N.key_depth; l++) {
+        PG_UNROLL
+        for (int j = 0; j < QB; j++) eb[j] = ld.at_byte(node_child_byte(eb[j], b[j]));
     }
     PG_UNROLL
-    for (int j = 0; j < QA; j++) ca[j] = e[j] & ~kLeaf;
+    for (int j = 0; j < QA; j++) ca[j] = (ea[j] >> 12) - N.ipself;
     PG_UNROLL
-    for (int j = 0; j < QB; j++) cb[j] = e[QA + j] & ~kLeaf;
+    for (int j = 0; j < QB; j++) cb[j] = (eb[j] >> 12) - N.kself;
 }
 
 #ifndef PG_NODE_WALK2  // node kernels: IPv4 and key tries in one lockstep walk
@@ -716,7 +700,7 @@ PG_HD void classify_node_q(const DevTableSet& T, const DevNode& N, const L& img,
     PG_UNROLL
     for (int j = 0; j < 2 * Q; j++) ipc[j] = ips[j] % N.n_ipc;
 #else
-    node_trie_q<PRED>(img, 0u, N.ip_s1, 32u, ips, ipc);
+    node_trie_q<PRED>(img, 0u, N.ip_s1, 32u, N.ip_depth, N.ipself, ips, ipc);
 #endif
     if (MODE == 2) {
         uint32_t keys[2 * Q], kc[2 * Q];
@@ -725,14 +709,14 @@ PG_HD void classify_node_q(const DevTableSet& T, const DevNode& N, const L& img,
             keys[j] = key[j] < kWalkKeyLimit ? key[j] : 0u;
             keys[Q + j] = kack[j] < kWalkKeyLimit ? kack[j] : 0u;
         }
-        node_trie_q<PRED>(img, N.key_root, N.key_k1, 18u, keys, kc);
+        node_trie_q<PRED>(img, N.key_root, N.key_k1, 18u, N.key_depth, N.kself, keys, kc);
         PG_UNROLL
         for (int j = 0; j < Q; j++) gs[j] = kc[j], ga[j] = kc[Q + j];
     } else {
         uint32_t keys[Q];
         PG_UNROLL
         for (int j = 0; j < Q; j++) keys[j] = key[j] < kWalkKeyLimit ? key[j] : 0u;
-        node_trie_q<PRED>(img, N.key_root, N.key_k1, 18u, keys, gs);
+        node_trie_q<PRED>(img, N.key_root, N.key_k1, 18u, N.key_depth, N.kself, keys, gs);
         PG_UNROLL
         for (int j = 0; j < Q; j++) ga[j] = gs[j];
     }

@@ -44,8 +44,11 @@ struct DevTable {          // 32 B: two 16-B loads
 // covers evaluated through one IPv4 trie and one L4-key trie shared by all tables, and one
 // cross-table entry per evaluation.
 //   img    u32[]  (tries: non-leaf entries in the node encoding, blobwalk.hpp node_entry)
-//                 IPv4 trie (root at word 0, leaf = node IP class) | L4-key trie (leaf = node
-//                 key class) | ipinfo uint2[n_ipc] {interface, tin | tout << 16} | tabinfo
+//                 IPv4 trie (root at word 0, leaf -> the node IP class's self word) | L4-key
+//                 trie (leaf -> the node key class's self word) | ipself u32[n_ipc] | kself
+//                 u32[gk] (self words: A << 10 at byte A, so a finished lookup re-reads itself
+//                 and every lookup has the trie's depth) | ipinfo uint2[n_ipc] {interface,
+//                 tin | tout << 16} | tabinfo
 //                 uint4[T] {cross base, nkc | covered << 31, common row, 0} | kmap u16[T][gk]
 //                 (local key class) | the words up to img_words_base are the base image;
 //                 then the common-row section (cmap != 0): per covered table its most
@@ -69,6 +72,10 @@ struct DevNode {
     uint32_t img_words_base;  // image without the common-row section
     uint32_t cmap;         // word offset of the common-row bitmap in img, 0 = none
     uint32_t ip_s1, key_root, key_k1;
+    // fixed-depth tries (blobwalk.hpp node_child_byte): a leaf points at its class's self word
+    // (IPv4: ipself + class, key: kself + class, word offsets in img); every lookup takes
+    // exactly ip_depth / key_depth reads
+    uint32_t ip_depth, key_depth, ipself, kself;
     uint32_t ipinfo, tabinfo, kmap;  // word offsets in img
     uint32_t gk;           // node key classes
     uint32_t n_ipc;        // node IP classes

@@ -570,6 +570,41 @@ bool build_fast_table(const DevRule* rules, uint32_t n, uint32_t rule_base, uint
     return true;
 }
 
+// ---- node tries: depth and fixed-depth leaves (kEncNode: child BYTE offset << 10) -------------
+namespace {
+uint32_t node_trie_depth(const std::vector<uint32_t>& b, uint32_t root, uint32_t s1) {
+    uint32_t d = 1;
+    struct J {
+        uint32_t at, n, depth;
+    };
+    std::vector<J> st{{root, 1u << s1, 1}};
+    while (!st.empty()) {
+        J j = st.back();
+        st.pop_back();
+        d = std::max(d, j.depth);
+        for (uint32_t e = 0; e < j.n; e++) {
+            const uint32_t v = b[j.at + e];
+            if (v & kLeaf) continue;
+            st.push_back({(v >> 10) / 4u, 1u << ((v >> 5) & 31u), j.depth + 1});
+        }
+    }
+    return d;
+}
+// leaves (kLeaf | class) -> pointers to self words (class c: word self0 + c)
+void node_point_leaves(std::vector<uint32_t>& b, uint32_t root, uint32_t s1, uint32_t self0) {
+    std::vector<std::pair<uint32_t, uint32_t>> st{{root, 1u << s1}};
+    while (!st.empty()) {
+        auto j = st.back();
+        st.pop_back();
+        for (uint32_t e = 0; e < j.second; e++) {
+            uint32_t& v = b[j.first + e];
+            if (v & kLeaf) v = ((self0 + (v & ~kLeaf)) * 4u) << 10;
+            else st.push_back({(v >> 10) / 4u, 1u << ((v >> 5) & 31u)});
+        }
+    }
+}
+}  // namespace
+
 // ---- FD blob: the fixed-depth form of a dst-independent CROSS table --------------------------
 // Layout (u32 words; trie entries hold WORD offsets, kEncWords, so a blob is < 16 MiB):
 //   [0] kFlagFD  [1] default verdict  [2] src root (16)  [3] s1  [4] key root  [5] k1
@@ -841,11 +876,37 @@ bool build_node(HostTableSet& h, const std::vector<TableAnalysis*>& an, const st
     // image: tries, ipinfo, tabinfo, kmap
     std::vector<uint32_t>& img = h.node_img;
     DevNode& N = h.node;
-    N.ip_s1 = std::min(pick_stride(gb.size(), 32, tu), tu.node_root_bits);
-    if (build_trie(img, gb, gcls, 32, N.ip_s1, tu, tu.lc_node != 0, kEncNode) != 0) return false;
+    // IPv4 trie root: the smallest trie among the root strides that give the fewest levels (a
+    // walk reads exactly depth words; a smaller image leaves LDS for the counter histogram --
+    // config 5: 12 -> 10 bits keeps image + histogram within two workgroups per CU)
+    {
+        const uint32_t top = std::min(pick_stride(gb.size(), 32, tu), tu.node_root_bits);
+        uint32_t best_d = ~0u;
+        std::vector<uint32_t> tmp;
+        for (uint32_t s1 = top; s1 + 4 > top && s1 >= 4; s1--) {
+            tmp.clear();
+            if (build_trie(tmp, gb, gcls, 32, s1, tu, tu.lc_node != 0, kEncNode) != 0) return false;
+            const uint32_t d = node_trie_depth(tmp, 0, s1);
+            if (d < best_d || (d == best_d && tmp.size() < img.size())) {
+                best_d = d;
+                N.ip_s1 = s1;
+                img.swap(tmp);
+            }
+        }
+    }
     N.key_k1 = std::min(pick_stride(kb.size(), 18, tu), tu.node_root_bits);
     N.key_root = build_trie(img, kb, kcls, 18, N.key_k1, tu, false, kEncNode);
     if (N.key_root == kTrieFail) return false;
+    // fixed depth: leaves -> self words of their classes (DevNode)
+    N.ip_depth = node_trie_depth(img, 0, N.ip_s1);
+    N.key_depth = node_trie_depth(img, N.key_root, N.key_k1);
+    N.ipself = (uint32_t)img.size();
+    for (uint32_t g = 0; g < G; g++) img.push_back(((N.ipself + g) * 4u) << 10);
+    N.kself = (uint32_t)img.size();
+    for (uint32_t g = 0; g < GK; g++) img.push_back(((N.kself + g) * 4u) << 10);
+    if ((uint64_t)img.size() * 4 >= kNodeChildMaxWords * 4ull) return false;
+    node_point_leaves(img, 0, N.ip_s1, N.ipself);
+    node_point_leaves(img, N.key_root, N.key_k1, N.kself);
     while (img.size() % 2) img.push_back(0);
     N.ipinfo = (uint32_t)img.size();
     for (uint32_t g = 0; g < G; g++) {
