@@ -525,6 +525,23 @@ void pg_vpptcp_txn_free(pg_vpptcp_txn* t);
 /* PolicyConfigurator.RegisterRenderer for the VPPTCP renderer */
 int pg_configurator_register_vpptcp(pg_configurator* c, pg_vpptcp_renderer* r);
 
+/* VPP's session-rule lookup on the device. Installs the session-rule table (scope PG's
+ * kScopeLocal = 2 with its application-namespace index, or kScopeGlobal = 1) of s into ctx as
+ * the ACL acl_name (a put, as by pg_apply_txn; call again after the table changed), so that
+ * pg_classify(ctx, PG_MODE_SINGLE, pg_table_id(ctx, acl_name), ...) classifies connections by
+ * it: the table's IPv4 rules (prefixes up to 32 bits) ordered most specific first (lcl_plen + rmt_plen + one per set
+ * port, ties in SessionRule.Compare order, session_rule.go:168-209) and first match, which is
+ * the containment order renderer/api.go:111-112 defines for the ContivRules they come from
+ * (convertContivRule, session_rule.go:263-361). Tuple fields: a local table keys on
+ * (src_ip = local address, dst_ip = remote address, dst_port = remote port), the global table
+ * on (src_ip = remote, dst_ip = local, dst_port = local port); proto TCP / UDP. Verdict PERMIT =
+ * ALLOW, DENY = DENY with the rule's slot, the ACL's default slot = no session rule applies.
+ * The reference has no session-rule lookup (VPP's own code): parity unpinned beyond the
+ * restatement in oracle/vpptcp.py. PG_EINVAL (+ pg_last_error) for a rule this form cannot
+ * hold: a port on the side the table does not key on, an action other than ALLOW / DENY. */
+int pg_session_table_install(pg_ctx* ctx, const pg_session_rules* s, int scope, uint32_t ns_index,
+                             const char* acl_name);
+
 #ifdef __cplusplus
 }
 #endif

@@ -106,6 +106,40 @@ def compare_ipnets_bytes(ap, a, bp, b) -> int:
     return P._bytes_compare(bytes(a), bytes(b))
 
 
+def _in_prefix(addr: int, ip: bytes, plen: int) -> bool:
+    if plen == 0:
+        return True
+    if plen > 32:  # an IPv4 rule with an IPv6-length prefix (mixed-family ContivRule)
+        return False
+    net = int.from_bytes(bytes(ip[:4]), "big")
+    m = (0xFFFFFFFF << (32 - plen)) & 0xFFFFFFFF
+    return (addr & m) == (net & m)
+
+
+def session_lookup(table, lcl_ip: int, lcl_port: int, rmt_ip: int, rmt_port: int, proto: int):
+    """VPP's session-rule lookup over one table (the product: pg_session_table_install): the
+    most specific IPv4 rule matching the connection -- specificity lcl_plen + rmt_plen + one
+    per set port, ties to the rule first in SessionRule.Compare order (with tag) -- or None.
+    A rule matches when its transport protocol is the packet's (proto: renderer.Protocol,
+    TCP 0 / UDP 1, as the ACL engine's packets carry it), both
+    addresses are inside its prefixes and each set port equals the packet's. VPP's own lookup
+    is not in the reference: parity unpinned beyond this restatement, which follows the
+    containment order renderer/api.go:111-112 gives the ContivRules the rules come from."""
+    want = {0: 0, 1: 1}.get(proto)  # renderer.Protocol TCP / UDP -> TransportProto
+    best = None
+    for r in table:
+        if not r.is_ip4 or want is None or r.transport_proto != want:
+            continue
+        if not (_in_prefix(lcl_ip, r.lcl_ip, r.lcl_plen) and _in_prefix(rmt_ip, r.rmt_ip, r.rmt_plen)):
+            continue
+        if (r.lcl_port and r.lcl_port != lcl_port) or (r.rmt_port and r.rmt_port != rmt_port):
+            continue
+        w = r.lcl_plen + r.rmt_plen + (r.lcl_port != 0) + (r.rmt_port != 0)
+        if best is None or w > best[0] or (w == best[0] and r.compare(best[1], True) < 0):
+            best = (w, r)
+    return None if best is None else best[1]
+
+
 class IPv4Net:
     """The renderer's IPv4Net dependency (session_rule.go:88-95), as the test's mock."""
 

@@ -221,6 +221,7 @@ _SIGS = {
     "pg_vpptcp_txn_commit": (C.c_int, [_P]),
     "pg_vpptcp_txn_free": (None, [_P]),
     "pg_configurator_register_vpptcp": (C.c_int, [_P, _P]),
+    "pg_session_table_install": (C.c_int, [_P, _P, C.c_int, C.c_uint32, C.c_char_p]),
 }
 EXPORTED = sorted(_SIGS)
 

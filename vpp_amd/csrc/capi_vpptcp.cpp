@@ -214,6 +214,33 @@ int pg_vpptcp_txn_commit(pg_vpptcp_txn* t) {
 }
 void pg_vpptcp_txn_free(pg_vpptcp_txn* t) { delete t; }
 
+int pg_session_table_install(pg_ctx* ctx, const pg_session_rules* s, int scope, uint32_t ns_index,
+                             const char* acl_name) {
+    if (!ctx || !s || !acl_name || !*acl_name) return PG_EINVAL;
+    if (scope != kScopeLocal && scope != kScopeGlobal) return PG_EINVAL;
+    try {
+        const std::vector<SessionRule>* t = s->t.table(scope, ns_index);
+        const std::vector<SessionRule> none;
+        std::string err;
+        ACLPtr acl = session_table_acl(t ? *t : none, scope, acl_name, &err);
+        if (!acl) {
+            ctx->eng.last_error = err;
+            return PG_EINVAL;
+        }
+        AclOps ops;
+        ops[acl_name] = acl;
+        err = ctx->eng.apply_txn(false, ops);
+        if (!err.empty()) {
+            ctx->eng.last_error = err;
+            return PG_EFAULT;
+        }
+        return PG_OK;
+    } catch (const std::exception& e) {
+        ctx->eng.last_error = e.what();
+        return PG_ENOMEM;
+    }
+}
+
 int pg_configurator_register_vpptcp(pg_configurator* c, pg_vpptcp_renderer* r) {
     if (!c || !r) return PG_EINVAL;
     c->c.renderers.push_back(r->r.get());

@@ -210,7 +210,9 @@ struct Hist {
     uint32_t* lds;
     unsigned long long* glob;
     PG_HD void inc(uint32_t slot) const {
-#if defined(__HIP_DEVICE_COMPILE__)
+#if defined(__HIP_DEVICE_COMPILE__) && defined(PG_PROBE_NOINC)  // measurement build only
+        if (slot == 0xFFFFFFFFu) lds[0] = 0;
+#elif defined(__HIP_DEVICE_COMPILE__)
         // One LDS (or global) atomic per lane. PG_AGG_ROUNDS > 0 first lets the lanes that
         // share the first active lane's slot (a reflective ACL's rule, "no ACL", a default
         // deny) add their count with one atomic, per round; A/B on MI355X with warmed-up

@@ -550,7 +550,9 @@ void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
         __syncthreads();
         for (uint32_t i = threadIdx.x; i < T.n_slots; i += BS) {
             const uint32_t v = hist[i];
+#if !defined(PG_PROBE_NOFLUSH)  // measurement build only: the histogram is not flushed
             if (v) atomicAdd(&counters[i], (unsigned long long)v);
+#endif
         }
     }
 }

@@ -216,6 +216,56 @@ void diff_rules(const ContivRuleTable& a, const ContivRuleTable& b, std::vector<
         if (!a.has_rule(r)) not_in_a->push_back(r);
 }
 
+// --- session-rule lookup as a first-match ACL ----------------------------------------------------
+static std::string v4_cidr(const uint8_t* ip, uint8_t plen) {
+    if (plen == 0) return std::string();  // 0/0: any address
+    return std::to_string(ip[0]) + "." + std::to_string(ip[1]) + "." + std::to_string(ip[2]) + "." +
+           std::to_string(ip[3]) + "/" + std::to_string(plen);
+}
+
+ACLPtr session_table_acl(const std::vector<SessionRule>& table, int scope, const std::string& name, std::string* err) {
+    std::vector<const SessionRule*> v;
+    for (const SessionRule& r : table)
+        // the engine classifies IPv4 packets; an IPv4 rule with a prefix longer than 32 bits (a
+        // global rule whose ContivRule mixes families, session_rule.go:280-297) matches none
+        if (r.is_ip4 && r.lcl_plen <= 32 && r.rmt_plen <= 32) v.push_back(&r);
+    auto weight = [](const SessionRule* r) {
+        return (int)r->lcl_plen + (int)r->rmt_plen + (r->lcl_port != 0) + (r->rmt_port != 0);
+    };
+    std::stable_sort(v.begin(), v.end(), [&](const SessionRule* a, const SessionRule* b) {
+        const int wa = weight(a), wb = weight(b);
+        if (wa != wb) return wa > wb;
+        return a->compare(*b, true) < 0;
+    });
+    const bool global = scope != kScopeLocal;
+    auto acl = std::make_shared<ACL>();
+    acl->name = name;
+    acl->ingress = {name};  // the ACL engine takes ACLs applied to an interface (its own name)
+    for (const SessionRule* r : v) {
+        // the key port: the remote one of a local table, the local one of the global table
+        if ((global && r->rmt_port) || (!global && r->lcl_port)) {
+            *err = "session rule port on the side the table does not key on";
+            return nullptr;
+        }
+        if (r->action_index != kSrActionAllow && r->action_index != kSrActionDeny) {
+            *err = "session rule action other than ALLOW / DENY";
+            return nullptr;
+        }
+        AclRule a;
+        a.action = r->action_index == kSrActionAllow ? kAclPermit : kAclDeny;
+        const std::string lcl = v4_cidr(r->lcl_ip, r->lcl_plen), rmt = v4_cidr(r->rmt_ip, r->rmt_plen);
+        a.src_network = global ? rmt : lcl;
+        a.dst_network = global ? lcl : rmt;
+        const uint16_t port = global ? r->lcl_port : r->rmt_port;
+        L4Section& s = r->transport_proto == kSrProtoUDP ? a.udp : a.tcp;
+        s.present = s.has_src = s.has_dst = true;
+        s.src = PortRange{0, 0xFFFF};
+        s.dst = port ? PortRange{port, port} : PortRange{0, 0xFFFF};
+        acl->rules.push_back(a);
+    }
+    return acl;
+}
+
 // --- VPP session-rule tables ----------------------------------------------------------------
 
 void SessionRuleTables::clear() {

@@ -87,6 +87,18 @@ struct SessionRuleTables {
                   const std::string& action) const;
 };
 
+// VPP's session-rule lookup over one table, as a first-match ACL the classification engine
+// compiles (pg_session_table_install): the table's IPv4 rules ordered most specific first --
+// specificity = lcl_plen + rmt_plen + one per specific port, ties in SessionRule::compare
+// order -- so a rule strictly inside another always precedes it (the containment order
+// renderer/api.go:111-112 gives ContivRules). Packet fields: a LOCAL table keys on (src = the
+// local address, dst = the remote address, dport = the remote port), the GLOBAL table on
+// (src = remote, dst = local, dport = local port), the other port is 0 (any) in every rule
+// convertContivRule emits (session_rule.go:263-361). No match = the ACL's default slot (VPP:
+// no session rule applies). nullptr + *err for a rule the form cannot hold (a port on the other
+// side, an action other than ALLOW / DENY).
+ACLPtr session_table_acl(const std::vector<SessionRule>& table, int scope, const std::string& name, std::string* err);
+
 struct VppTcpRenderer : CfgRenderer {
     const AppNsIndex* ipv4net;
     SessionRuleTables* vpp;

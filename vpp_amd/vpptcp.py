@@ -199,3 +199,21 @@ class Txn:
         if getattr(self, "h", None) and lib is not None:
             lib.pg_vpptcp_txn_free(self.h)
             self.h = None
+
+
+# --- session-rule lookup on the device (pg_session_table_install) --------------------------------
+def InstallSessionTable(engine, vpp, scope, nsIndex, aclName):
+    """VPP's session-rule table (ScopeLocal + nsIndex, or ScopeGlobal) of ``vpp`` installed in
+    ``engine`` as the ACL ``aclName``; returns its table id for SINGLE-mode classification.
+    Tuple fields per scope: ``SessionTuples``."""
+    engine._ck(lib.pg_session_table_install(engine.h, vpp.h, scope, nsIndex, _b(aclName)))
+    return engine.table_id(aclName)
+
+
+def SessionTuples(scope, lcl_ip, lcl_port, rmt_ip, rmt_port):
+    """(src_ip, dst_ip, dst_port) of connections looked up in a table of ``scope``: a local
+    table keys on (local address, remote address, remote port), the global table on (remote
+    address, local address, local port)."""
+    if scope == ScopeLocal:
+        return lcl_ip, rmt_ip, rmt_port
+    return rmt_ip, lcl_ip, lcl_port
