@@ -409,8 +409,9 @@ struct NodeEval {
             cm[j] = CM && (cw & 1u);
             pos[j] = cm[j] ? ti.z + lk : ti.x + ca[j] * (ti.y & 0xFFFFu) + lk;
             fb[j] = act[j] && !on[j];
-            // PAIR table (kNodePairFlag): the pair map entry first, its verdict row after
-            pr[j] = on[j] && (ti.y & kNodePairFlag);
+            // PAIR table (kNodePairFlag): the pair map entry first, its verdict row after (a
+            // uniform test first: node sets without PAIR tables skip this code)
+            pr[j] = N.n_pair && on[j] && (ti.y & kNodePairFlag);
             if (pr[j]) {
                 const uint32_t mo = ti.w & 0xFFFFu;
                 const uint32_t sc = img.u32(mo + ca[j]) & 0xFFFFu, dc = img.u32(mo + cb[j]) >> 16;
@@ -428,9 +429,11 @@ struct NodeEval {
             if (!cm[j]) w[j] = X.u32(pos[j]);
 #endif
         }
-        PG_UNROLL
-        for (int j = 0; j < Q; j++)
-            if (pr[j]) w[j] = X.u32(pv[j] + w[j] * pk[j]);
+        if (N.n_pair) {
+            PG_UNROLL
+            for (int j = 0; j < Q; j++)
+                if (pr[j]) w[j] = X.u32(pv[j] + w[j] * pk[j]);
+        }
         if (CM) {
             PG_UNROLL
             for (int j = 0; j < Q; j++)

@@ -360,8 +360,8 @@ __device__ __forceinline__ void stream_store(V v, V* p) {
 #ifndef PG_QCONN
 #define PG_QCONN 1
 #endif
-#ifndef PG_QCONN_COUNT  // CONN with hit counters (A/B on MI355X, config 5: 2 = +9 % over 1, 4 = -6 %)
-#define PG_QCONN_COUNT 2
+#ifndef PG_QCONN_COUNT  // CONN with hit counters (A/B on MI355X, config 5: 2 = +9 % over 1, 4 = -6 % in
+#define PG_QCONN_COUNT 1  // round 1; after the fixed-depth node walks 1 = +3.5 % over 2, tune1)
 #endif
 #ifndef PG_QSINGLE_FD  // SINGLE over an LDS-staged FD table (STAGE 4)
 #define PG_QSINGLE_FD 1

@@ -79,6 +79,7 @@ struct DevNode {
     uint32_t ipinfo, tabinfo, kmap;  // word offsets in img
     uint32_t gk;           // node key classes
     uint32_t n_ipc;        // node IP classes
+    uint32_t n_pair;       // covered PAIR tables (0: the evaluations skip the PAIR steps)
 };
 
 struct DevTableSet {       // device pointers (valid on the GPU)

@@ -931,6 +931,7 @@ bool build_node(HostTableSet& h, const std::vector<TableAnalysis*>& an, const st
     if (img.size() >= 0xFFFFu) return false;  // map offsets are 16-bit (tabinfo.w)
     N.gk = GK;
     N.n_ipc = G;
+    N.n_pair = (uint32_t)PC;
     N.img_words = N.img_words_base = (uint32_t)img.size();
     N.cmap = 0;
 
