@@ -395,6 +395,17 @@ int pg_mock_renderer_rules(pg_mock_renderer* r, const char* ns, const char* name
 int pg_mock_renderer_test_traffic(pg_mock_renderer* r, const char* ns, const char* name, int direction,
                                   const char* src_ip, const char* dst_ip, int protocol, uint16_t src_port,
                                   uint16_t dst_port);
+/* TestTraffic on the device: the pod's ingress (direction 0) / egress (1) list of r installed
+ * in ctx as the ACL acl_name (a put, as by pg_apply_txn; again after a new Commit), so that
+ * pg_classify(ctx, PG_MODE_SINGLE, pg_table_id(ctx, acl_name), ...) answers TestTraffic for
+ * a batch: PERMIT = AllowedTraffic, DENY = DeniedTraffic (with the rule's slot), the ACL's
+ * default slot = UnmatchedTraffic. Tuples carry the ContivRule protocol (TCP 0 / UDP 1 /
+ * OTHER 2) and the destination port; TestTraffic's source-port test needs no field because
+ * the configurator never sets a rule's source port -- a list that has one (or a protocol-OTHER
+ * rule) is refused with PG_EINVAL. PG_ENOENT: the pod was not rendered (TestTraffic:
+ * UnmatchedTraffic for every packet). */
+int pg_mock_renderer_install(pg_ctx* ctx, const pg_mock_renderer* r, const char* ns, const char* name, int direction,
+                             const char* acl_name);
 
 /* ---- K8s policy cache and processor ------------------------------
  * The KSR objects cross the boundary in their protobuf wire form (proto.Marshal of

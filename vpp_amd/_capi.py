@@ -222,6 +222,7 @@ _SIGS = {
     "pg_vpptcp_txn_free": (None, [_P]),
     "pg_configurator_register_vpptcp": (C.c_int, [_P, _P]),
     "pg_session_table_install": (C.c_int, [_P, _P, C.c_int, C.c_uint32, C.c_char_p]),
+    "pg_mock_renderer_install": (C.c_int, [_P, _P, C.c_char_p, C.c_char_p, C.c_int, C.c_char_p]),
 }
 EXPORTED = sorted(_SIGS)
 

@@ -140,6 +140,26 @@ class MockRenderer:
             raise R.PolicyError(rc, "TestTraffic")
         return rc
 
+    def InstallTraffic(self, engine, pod, direction, aclName):
+        """TestTraffic on the device: the pod's ingress / egress list installed in ``engine`` as
+        the ACL ``aclName``; returns its table id (None: the pod was not rendered, every packet
+        UnmatchedTraffic). Verdicts of pg_classify SINGLE on it: ``TrafficOf``."""
+        ns, name = (_b(v) for v in R._pod(pod))
+        rc = lib.pg_mock_renderer_install(engine.h, self.h, ns, name, direction, _b(aclName))
+        if rc == _capi.PG_ENOENT:
+            return None
+        engine._ck(rc)
+        return engine.table_id(aclName)
+
+    @staticmethod
+    def TrafficOf(engine, table_id, verdicts):
+        """verdict words of a TestTraffic table -> TrafficAction (Denied 0, Allowed 1,
+        Unmatched 2)"""
+        import numpy as np
+        v = np.asarray(verdicts, np.uint32)
+        act = np.where((v >> 30) == 1, 1, 0)
+        return np.where((v & 0x3FFFFFFF) == engine.slot_of_rule(table_id, -1), 2, act)
+
     def __del__(self):
         if getattr(self, "h", None) and lib is not None:
             lib.pg_mock_renderer_free(self.h)

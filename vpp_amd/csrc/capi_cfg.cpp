@@ -169,4 +169,29 @@ int pg_mock_renderer_test_traffic(pg_mock_renderer* r, const char* ns, const cha
     return r->r.test_traffic(PodID{ns, name}, direction, s, d, protocol, src_port, dst_port);
 }
 
+int pg_mock_renderer_install(pg_ctx* ctx, const pg_mock_renderer* r, const char* ns, const char* name, int direction,
+                             const char* acl_name) {
+    if (!ctx || !r || !ns || !name || !acl_name || !*acl_name) return PG_EINVAL;
+    try {
+        std::string err;
+        bool missing = false;
+        ACLPtr acl = r->r.traffic_acl(PodID{ns, name}, direction, acl_name, &err, &missing);
+        if (!acl) {
+            ctx->eng.last_error = err;
+            return missing ? PG_ENOENT : PG_EINVAL;
+        }
+        AclOps ops;
+        ops[acl_name] = acl;
+        err = ctx->eng.apply_txn(false, ops);
+        if (!err.empty()) {
+            ctx->eng.last_error = err;
+            return PG_EFAULT;
+        }
+        return PG_OK;
+    } catch (const std::exception& e) {
+        ctx->eng.last_error = e.what();
+        return PG_ENOMEM;
+    }
+}
+
 }  // extern "C"

@@ -93,6 +93,38 @@ int MockRenderer::test_traffic(const PodID& pod, int direction, const Bytes& src
     return kUnmatchedTraffic;
 }
 
+ACLPtr MockRenderer::traffic_acl(const PodID& pod, int direction, const std::string& name, std::string* err,
+                                 bool* missing) const {
+    *missing = false;
+    auto it = config.find(pod);
+    if (it == config.end()) {
+        *missing = true;
+        *err = "pod not rendered";
+        return nullptr;
+    }
+    auto acl = std::make_shared<ACL>();
+    acl->name = name;
+    acl->ingress = {name};
+    for (const ContivRule& r : direction == kIngressTraffic ? it->second.ingress : it->second.egress) {
+        if (r.protocol == kOTHER || (r.protocol != kANY && r.src_port != 0)) {
+            *err = "rule with protocol OTHER or a source port";
+            return nullptr;
+        }
+        AclRule a;
+        a.action = r.action == kPermit ? kAclPermit : kAclDeny;
+        if (r.src.ip.len > 0) a.src_network = ipnet_string(r.src);
+        if (r.dst.ip.len > 0) a.dst_network = ipnet_string(r.dst);
+        if (r.protocol == kTCP || r.protocol == kUDP) {
+            L4Section& l4 = r.protocol == kTCP ? a.tcp : a.udp;
+            l4.present = l4.has_src = l4.has_dst = true;
+            l4.src = PortRange{0, 0xFFFF};
+            l4.dst = r.dst_port ? PortRange{r.dst_port, r.dst_port} : PortRange{0, 0xFFFF};
+        }
+        acl->rules.push_back(a);
+    }
+    return acl;
+}
+
 // ---- configurator ---------------------------------------------------------------------
 PolicyConfiguratorTxn::PolicyConfiguratorTxn(PolicyConfigurator* c, bool rs) : cfg(c), resync(rs) {
     if (!resync) pod_ip_addresses = cfg->pod_ip_addresses;  // configurator_impl.go:119-124

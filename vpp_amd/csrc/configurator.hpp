@@ -92,6 +92,14 @@ struct MockRenderer : CfgRenderer {
     std::unique_ptr<CfgRendererTxn> new_txn(bool resync) override;
     int test_traffic(const PodID& pod, int direction, const Bytes& src, const Bytes& dst, int protocol,
                      uint16_t src_port, uint16_t dst_port) const;
+    // TestTraffic on the device (pg_mock_renderer_install): the pod's ingress / egress list as a
+    // first-match ACL named `name` (applied to an interface of that name, as the ACL engine
+    // wants). A TCP / UDP rule matches its protocol and destination port (0 = any), an ANY rule
+    // every packet, its ports ignored -- TestTraffic's semantics; the ACL's default slot =
+    // UnmatchedTraffic. nullptr + *err: pod not rendered (*missing), or a rule this form cannot
+    // hold (a source port, protocol OTHER; the configurator emits neither).
+    ACLPtr traffic_acl(const PodID& pod, int direction, const std::string& name, std::string* err,
+                       bool* missing) const;
 };
 
 struct PolicyConfigurator {
