@@ -172,11 +172,13 @@ def main():
     }
     if allreduce is not None:
         line.update(allreduce)
-    # the same fraction against what a plain device copy reaches on this GPU (after the timed
-    # region): read + write of a 1 GiB buffer
-    cp, rd = stream_peaks_gbps()
-    line["roofline"]["measured_stream_gbps"] = {"copy": cp, "read": rd}
-    line["roofline"]["frac_of_measured_stream"] = round(achieved / max(cp, rd), 4)
+    # the same fraction against what moving this launch's own bytes reaches on this GPU (after
+    # the timed region): pg_stream_probe issues the classify launch's loads and store over the
+    # same batch without the classification; torch's 1 GiB device copy beside it
+    probe = stream_ceiling_gbps(e, w, b, out, bpt, a.steps)
+    cp = torch_copy_gbps()
+    line["roofline"]["measured_stream_gbps"] = {"probe": probe, "copy": cp}
+    line["roofline"]["frac_of_measured_stream"] = round(achieved / probe, 4)
     if rank == 0 and world == 1 and not a.no_cpu:
         line["cpu_baseline"], line["parity_sample"] = cpu_baseline(w, b, out, a.cpu_sample, a.faithful_seconds,
                                                                    a.cpu_seconds)
@@ -263,29 +265,37 @@ def dry_run(a, rank, world):
         dist.destroy_process_group()
 
 
-def stream_peaks_gbps(nbytes=1 << 30, reps=10):
-    """measured HBM stream rates on this GPU (torch's own kernels, median of reps): a
-    device-to-device copy (bytes read + written / time) and a read-only fp32 sum (bytes read /
-    time); the classify kernels read 7-13 B and write 4 B per tuple, between the two"""
+def _median_ms(fn, reps):
+    fn()
+    ts = []
+    for _ in range(reps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        fn()
+        e1.record()
+        torch.cuda.synchronize()
+        ts.append(e0.elapsed_time(e1))
+    return sorted(ts)[len(ts) // 2]
+
+
+def stream_ceiling_gbps(e, w, b, out, bpt, reps):
+    """pg_stream_probe over the timed batch: the loads of exactly the fields the classify launch
+    reads (dst unless the table is dst-free, sport in CONN mode) and its verdict store, with
+    the same vector widths and grid; algorithmic bytes / median launch time"""
+    fields = (0 if bpt == 11 and w.mode == 0 else 1) | (2 if w.mode == 2 else 0)
+    sink = torch.empty_like(out)  # the verdicts in `out` are checked against the CPU oracle later
+    ms = _median_ms(lambda: D.stream_probe(e, fields, b, sink), max(reps, 5))
+    del sink
+    return round(b.n * bpt / (ms * 1e-3) / 1e9, 1)
+
+
+def torch_copy_gbps(nbytes=1 << 30, reps=10):
+    """torch's own device-to-device copy of a 1 GiB buffer (bytes read + written / time)"""
     x = torch.ones(nbytes // 4, dtype=torch.float32, device="cuda")
     y = torch.empty_like(x)
-
-    def med(fn):
-        fn()
-        ts = []
-        for _ in range(reps):
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
-            fn()
-            e1.record()
-            torch.cuda.synchronize()
-            ts.append(e0.elapsed_time(e1))
-        return sorted(ts)[len(ts) // 2] * 1e-3
-
-    copy = 2 * nbytes / med(lambda: y.copy_(x)) / 1e9
-    read = nbytes / med(lambda: x.sum()) / 1e9
+    ms = _median_ms(lambda: y.copy_(x), reps)
     del x, y
-    return round(copy, 1), round(read, 1)
+    return round(2 * nbytes / (ms * 1e-3) / 1e9, 1)
 
 
 def bytes_per_tuple(w):
@@ -374,6 +384,14 @@ def cpu_baseline(w, b, out, k, faithful_s=8.0, budget_s=10.0):
         visited = np.where(idx >= 0, idx.astype(np.int64) + 1, nr)
         extra["reference_rules_visited"] = {"mean": round(float(visited.mean()), 1),
                                             "p99": int(np.percentile(visited, 99)), "rules": nr}
+        # ... and the loads the GPU walk makes of the compiled structure per tuple (the kernels'
+        # walk code on the host with counting loaders), LDS-staged vs gathered from HBM / L2
+        ks = min(k, 1 << 20)
+        nl, nm, stage = e.debug_walk_stats(w.table_id, src[:ks], dst[:ks], dport[:ks], proto[:ks])
+        extra["gpu_loads_per_tuple"] = {"lds_mean": round(float(nl.mean()), 3),
+                                        "gather_mean": round(float(nm.mean()), 3),
+                                        "gather_p99": int(np.percentile(nm, 99)), "gather_max": int(nm.max()),
+                                        "stage": stage, "sample": ks}
         faithful_ok = bool(((got[:kf] >> 30) == fa.astype(np.uint32)).all() and ((got[:kf] & 0x3FFFFFFF) == fslot).all())
     else:
         wd = world.World(e, w.local_ifs, w.node_if)

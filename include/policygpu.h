@@ -236,6 +236,14 @@ int pg_debug_walk_blob(pg_ctx* ctx, const char* acl_name, const uint32_t* src, c
  * Does not touch the device. */
 int pg_debug_classify_host(pg_ctx* ctx, int mode, int table_id, const pg_tuple_soa* tuples, uint64_t n,
                            uint32_t* out, uint64_t* counters, int flags);
+/* TESTS / MEASUREMENT ONLY -- never on the classify path: per tuple, the loads a SINGLE-mode
+ * launch on table_id makes of the table's classification structure, split by where the launch
+ * finds the word: lds_reads (the LDS-staged part) and mem_reads (HBM / L2 gathers; rule reads of
+ * the linear scan for ANY-protocol packets). *stage = the staging the launch uses (device.hip
+ * k_classify STAGE: 0 none, 1 blob, 2 src root, 4 FD blob, 5 FD prefix). Runs the kernels' walk
+ * code on the host with counting loaders; does not touch the device. */
+int pg_debug_walk_stats(pg_ctx* ctx, int table_id, const pg_tuple_soa* tuples, uint64_t n, uint32_t* lds_reads,
+                        uint32_t* mem_reads, int* stage);
 /* node classifier (PERPOD / CONN) size: IPv4 classes, L4-key classes, LDS image bytes,
  * cross-table bytes; PG_ENOENT when it was not built */
 int pg_node_stats(pg_ctx* ctx, uint32_t* ip_classes, uint32_t* key_classes, uint64_t* image_bytes,
@@ -247,6 +255,15 @@ int pg_node_common_stats(pg_ctx* ctx, uint64_t* base_image_bytes, uint64_t* comm
 /* reference-shaped linear-scan kernel (K1) on one table, for validation and comparison */
 int pg_classify_linear(pg_ctx* ctx, int table_id, const pg_tuple_soa* tuples, uint64_t n, uint32_t* out,
                        void* hip_stream);
+/* MEASUREMENT -- not part of the reference's interface: the stream ceiling of a pg_classify
+ * launch. Issues exactly the loads a launch makes of the tuple fields (src, dst_port, proto;
+ * dst_ip when fields & 1, src_port when fields & 2) and its 4-B store per tuple, with the same
+ * vector widths and grid, but no classification (out[i] = xor of the fields). bench.py times
+ * it beside the classify kernel: classify rate / probe rate = how close the classification
+ * comes to what moving its own bytes costs on this GPU. Fields and out must be vector-aligned
+ * (16-B src / dst / out); PG_EIO otherwise. */
+int pg_stream_probe(pg_ctx* ctx, int fields, const pg_tuple_soa* tuples, uint64_t n, uint32_t* out,
+                    void* hip_stream);
 /* device-resident per-rule hit counters (u64, pg_num_counter_slots entries) */
 uint64_t* pg_counters_device(pg_ctx* ctx);
 int pg_reset_counters(pg_ctx* ctx, void* hip_stream);

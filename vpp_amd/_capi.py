@@ -193,6 +193,9 @@ _SIGS = {
     "pg_policy_processor_process": (C.c_int, [_P, C.c_int, C.POINTER(C.c_char_p), C.c_size_t]),
     "pg_policy_processor_last_error": (C.c_char_p, [_P]),
     "pg_classify_linear": (C.c_int, [_P, C.c_int, C.POINTER(pg_tuple_soa), C.c_uint64, _P, _P]),
+    "pg_debug_walk_stats": (C.c_int, [_P, C.c_int, C.POINTER(pg_tuple_soa), C.c_uint64, C.POINTER(C.c_uint32),
+                                      C.POINTER(C.c_uint32), C.POINTER(C.c_int)]),
+    "pg_stream_probe": (C.c_int, [_P, C.c_int, C.POINTER(pg_tuple_soa), C.c_uint64, _P, _P]),
     "pg_counters_device": (_P, [_P]),
     "pg_reset_counters": (C.c_int, [_P, _P]),
     "pg_read_counters": (C.c_int, [_P, C.POINTER(C.c_uint64), C.c_size_t]),

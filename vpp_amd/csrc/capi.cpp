@@ -532,6 +532,83 @@ int pg_debug_walk_blob(pg_ctx* ctx, const char* acl_name, const uint32_t* src, c
 }  // extern "C"
 
 namespace {
+// A host loader that counts the reads of a walk by where the launch would find the word: in
+// the LDS-staged part of the blob, or in HBM / L2 (a gather). u2 / u4 reads count once (one
+// load instruction per lane on the device).
+struct CountingLoader {
+    const uint32_t* b;
+    bool lds;
+    uint32_t* n_lds;
+    uint32_t* n_mem;
+    void hit() const { ++*(lds ? n_lds : n_mem); }
+    uint32_t u32(uint32_t i) const { return hit(), b[i]; }
+    uint32_t at_byte(uint32_t off) const { return hit(), b[off >> 2]; }
+    W2 u2(uint32_t i) const { return hit(), W2{b[i], b[i + 1]}; }
+    W4 u4(uint32_t i) const { return hit(), W4{b[i], b[i + 1], b[i + 2], b[i + 3]}; }
+};
+}  // namespace
+
+extern "C" {
+int pg_debug_walk_stats(pg_ctx* ctx, int table_id, const pg_tuple_soa* t, uint64_t n, uint32_t* lds_reads,
+                        uint32_t* mem_reads, int* stage) {
+    if (!ctx || !t || (n && (!t->src_ip || !t->dst_ip || !t->dst_port || !t->proto || !lds_reads || !mem_reads)))
+        return PG_EINVAL;
+    GUARD_BEGIN
+    Engine& E = ctx->eng;
+    if (!E.compiled) E.compile();
+    if (table_id < 0 || (uint32_t)table_id >= E.host.tabs.size()) return fail(ctx, PG_EINVAL, "table id out of range");
+    const DevTable& hd = E.host.tabs[table_id];
+    const Tuning& tu = E.tune;
+    const uint32_t words = E.host.blob_words[table_id], prefix = E.host.blob_prefix[table_id];
+    const uint32_t root_words = (kSrcRoot + (1u << ((hd.fsk >> 8) & 0xFFu)) + 3u) & ~3u;
+    const bool linear = (hd.fsk & kFlagLinear) != 0;
+    // the launch device.hip launch_classify picks for this table (SINGLE mode)
+    int st = 0;
+    if (hd.fsk & kFlagFD) st = words <= tu.stage_max_words ? 4 : (prefix <= tu.stage_root_max_words ? 5 : 0);
+    else if (!linear && words && words <= tu.stage_max_words) st = 1;
+    else if (!linear && words && root_words <= tu.stage_root_max_words) st = 2;
+    if (stage) *stage = st;
+    const uint32_t* blob = E.host.blobs.data() + hd.blob_off;
+    for (uint64_t i = 0; i < n; i++) {
+        uint32_t nl = 0, nm = 0;
+        const uint32_t s = t->src_ip[i], d = t->dst_ip[i];
+        const uint32_t key = t->proto[i] > 2 ? kKeyANY : pkt_key_host(t->proto[i], t->dst_port[i]);
+        bool scan = linear || key >= kWalkKeyLimit;
+        if (!linear && !scan) {
+            const CountingLoader whole{blob, st == 1 || st == 4, &nl, &nm};
+            if (hd.fsk & kFlagFD) {
+                const CountingLoader lp{blob, true, &nl, &nm};
+                const uint32_t s1[1] = {s}, k1[1] = {key};
+                uint32_t w1[1];
+                if (st == 5) fd_walk(lp, CountingLoader{blob, false, &nl, &nm}, hd.fsk, hd.kroot, hd.xoff, hd.nkc, s1, k1, w1);
+                else fd_walk(whole, whole, hd.fsk, hd.kroot, hd.xoff, hd.nkc, s1, k1, w1);
+            } else {
+                const CountingLoader ld[1] = {whole};
+                const CountingLoader ld0[1] = {CountingLoader{blob, st != 0, &nl, &nm}};
+                const BlobTab tb[1] = {BlobTab{hd.fsk, hd.dflt, hd.kroot, hd.xoff, hd.nkc}};
+                const bool on[1] = {true};
+                const uint32_t s1[1] = {s}, d1[1] = {d}, k1[1] = {key};
+                uint32_t w1[1];
+                blob_walk(ld, ld0, tb, on, s1, d1, k1, w1);
+            }
+        }
+        if (scan) {  // the linear scan: one rule read per rule visited
+            for (uint32_t r = 0; r < hd.n_rules; r++) {
+                nm++;
+                const DevRule& R = E.host.rules[hd.rule_base + r];
+                if ((s & R.smask) != R.snet || (d & R.dmask) != R.dnet) continue;
+                if (key >= kKeyANY ? (R.act >> 4) != kActNever : (key >= R.klo && key <= R.khi)) break;
+            }
+        }
+        lds_reads[i] = nl;
+        mem_reads[i] = nm;
+    }
+    return PG_OK;
+    GUARD_END(ctx)
+}
+}  // extern "C"
+
+namespace {
 // host view of the compiled table set (pointers into the host image)
 DevTableSet host_view(const HostTableSet& h) {
     DevTableSet v{};
@@ -686,6 +763,22 @@ int pg_classify_linear(pg_ctx* ctx, int table_id, const pg_tuple_soa* t, uint64_
     std::string err;
     if (dev_classify_linear(T, table_id, t->src_ip, t->dst_ip, t->dst_port, t->proto, n, out, stream, &err) != 0 ||
         dev_mark_use(ctx->eng.cur, stream, &err) != 0)
+        return fail(ctx, PG_EIO, err);
+    return PG_OK;
+    GUARD_END(ctx)
+}
+
+int pg_stream_probe(pg_ctx* ctx, int fields, const pg_tuple_soa* t, uint64_t n, uint32_t* out, void* stream) {
+    if (!ctx || !t || fields < 0 || fields > 3) return PG_EINVAL;
+    DEVICE_GUARD(ctx);
+    GUARD_BEGIN
+    if (n == 0) return PG_OK;
+    if (!out || !t->src_ip || !t->dst_port || !t->proto || ((fields & 1) && !t->dst_ip) ||
+        ((fields & 2) && !t->src_port))
+        return fail(ctx, PG_EINVAL, "missing tuple field");
+    std::string err;
+    if (dev_stream_probe(ctx->eng.tune, fields, t->src_ip, t->dst_ip, t->src_port, t->dst_port, t->proto, n, out,
+                         stream, &err) != 0)
         return fail(ctx, PG_EIO, err);
     return PG_OK;
     GUARD_END(ctx)

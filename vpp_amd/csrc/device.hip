@@ -557,6 +557,39 @@ void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
     }
 }
 
+// Stream probe (measurement): exactly the loads and the store of a k_classify launch over the
+// same batch -- src, dport, proto (+ dst when DST, + sport when SP), P tuples per lane with
+// 16/8/4-byte non-temporal loads, one 16-byte verdict store -- with a 1-instruction "verdict"
+// instead of the classification. Its rate is the ceiling a classify launch of that byte mix
+// can reach on this GPU (bench.py frac_of_stream_ceiling).
+template <bool DST, bool SP, int BS>
+__global__ __launch_bounds__(BS) void k_stream_probe(const uint32_t* __restrict__ src, const uint32_t* __restrict__ dst,
+                                                     const uint16_t* __restrict__ sport,
+                                                     const uint16_t* __restrict__ dport,
+                                                     const uint8_t* __restrict__ proto, uint64_t n,
+                                                     uint32_t* __restrict__ out) {
+    constexpr int P = PG_TPL;
+    const uint64_t stride = (uint64_t)gridDim.x * BS;
+    const uint64_t first = (uint64_t)blockIdx.x * BS + threadIdx.x;
+    const uint64_t nfull = n / P;
+    for (uint64_t q = first; q < nfull; q += stride) {
+        const uint64_t i0 = q * P;
+        const Words<P> s = ld_words<P>(src + i0);
+        const Words<P> d = DST ? ld_words<P>(dst + i0) : Words<P>{};
+        const Words<P / 2> dp = ld_words<P / 2>(reinterpret_cast<const uint32_t*>(dport + i0));
+        const Words<P / 2> sp = SP ? ld_words<P / 2>(reinterpret_cast<const uint32_t*>(sport + i0)) : Words<P / 2>{};
+        const Words<P / 4> pr = ld_words<P / 4>(reinterpret_cast<const uint32_t*>(proto + i0));
+        Words<P> o;
+#pragma unroll
+        for (int j = 0; j < P; j++)
+            o.w[j] = s.w[j] ^ d.w[j] ^ (dp.w[j / 2] >> (16 * (j & 1))) ^ (sp.w[j / 2] >> (16 * (j & 1))) ^
+                     (pr.w[j / 4] >> (8 * (j & 3)));
+        st_words<P>(o, out + i0);
+    }
+    for (uint64_t i = nfull * P + first; i < n; i += stride)
+        out[i] = src[i] ^ (DST ? dst[i] : 0u) ^ dport[i] ^ (SP ? (uint32_t)sport[i] : 0u) ^ proto[i];
+}
+
 // K1: reference-shaped linear scan, one lane per tuple, rules wave-uniform
 __global__ __launch_bounds__(kBlock) void k_linear(DevTableSet T, uint32_t t, const uint32_t* __restrict__ src,
                                                    const uint32_t* __restrict__ dst,
@@ -850,6 +883,34 @@ int dev_classify_linear(const DevTableSet& T, int table_id, const uint32_t* src,
     if (n == 0) return 0;
     hipLaunchKernelGGL(k_linear, dim3(grid_for(n)), dim3(kBlock), 0, (hipStream_t)stream, T, (uint32_t)table_id,
                        src, dst, dport, proto, n, out);
+    HIPCHK(hipGetLastError());
+    return 0;
+}
+
+template <bool DST, bool SP>
+static void launch_probe(const Tuning& tu, const uint32_t* src, const uint32_t* dst, const uint16_t* sport,
+                         const uint16_t* dport, const uint8_t* proto, uint64_t n, uint32_t* out, hipStream_t st) {
+    auto k = k_stream_probe<DST, SP, 512>;
+    hipLaunchKernelGGL(k, dim3(grid_resident(k, 512, 0, (n + PG_TPL - 1) / PG_TPL, tu.blocks_per_cu)), dim3(512), 0,
+                       st, src, dst, sport, dport, proto, n, out);
+}
+
+int dev_stream_probe(const Tuning& tu, int fields, const uint32_t* src, const uint32_t* dst, const uint16_t* sport,
+                     const uint16_t* dport, const uint8_t* proto, uint64_t n, uint32_t* out, void* stream,
+                     std::string* err) {
+    if (n == 0) return 0;
+    auto al = [](const void* p, uintptr_t a) { return ((uintptr_t)p & (a - 1)) == 0; };
+    constexpr uintptr_t kPort = 2 * PG_TPL > 16 ? 16 : 2 * PG_TPL, kProto = PG_TPL > 16 ? 16 : PG_TPL;
+    if (!(al(src, 16) && al(dport, kPort) && al(proto, kProto) && al(out, 16) && (!(fields & 1) || al(dst, 16)) &&
+          (!(fields & 2) || al(sport, kPort)))) {
+        if (err) *err = "stream probe: tuple fields / output not vector-aligned";
+        return -1;
+    }
+    hipStream_t st = (hipStream_t)stream;
+    if (fields == 0) launch_probe<false, false>(tu, src, dst, sport, dport, proto, n, out, st);
+    else if (fields == 1) launch_probe<true, false>(tu, src, dst, sport, dport, proto, n, out, st);
+    else if (fields == 2) launch_probe<false, true>(tu, src, dst, sport, dport, proto, n, out, st);
+    else launch_probe<true, true>(tu, src, dst, sport, dport, proto, n, out, st);
     HIPCHK(hipGetLastError());
     return 0;
 }

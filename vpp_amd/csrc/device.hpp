@@ -206,6 +206,10 @@ int dev_classify(const DevTableSet& T, const Tuning& tu, int mode, int table_id,
 int dev_classify_linear(const DevTableSet& T, int table_id, const uint32_t* src, const uint32_t* dst,
                         const uint16_t* dport, const uint8_t* proto, uint64_t n, uint32_t* out, void* stream,
                         std::string* err);
+// the stream ceiling of a classify launch: its loads (fields: 1 = dst, 2 = sport) and store only
+int dev_stream_probe(const Tuning& tu, int fields, const uint32_t* src, const uint32_t* dst, const uint16_t* sport,
+                     const uint16_t* dport, const uint8_t* proto, uint64_t n, uint32_t* out, void* stream,
+                     std::string* err);
 int dev_gen(const DevTableSet& T, const GenParams& g, uint64_t n, uint32_t* src, uint32_t* dst, uint16_t* sport,
             uint16_t* dport, uint8_t* proto, void* stream, std::string* err);
 int dev_conn_queries(const DevTableSet& T, const ConnQueryDev* q_host, size_t n, uint32_t* out_host,

@@ -97,6 +97,13 @@ def classify_linear(engine, table_id, batch, out, stream=None):
                                       _stream_ptr(stream)))
 
 
+def stream_probe(engine, fields, batch, out, stream=None):
+    """pg_stream_probe: the loads and store of a classify launch over `batch` without the
+    classification (fields: 1 = dst, 2 = sport) -- a measurement, not a classification"""
+    soa = batch.soa()
+    engine._ck(lib.pg_stream_probe(engine.h, fields, C.byref(soa), batch.n, out.data_ptr(), _stream_ptr(stream)))
+
+
 def counters_device_ptr(engine):
     p = lib.pg_counters_device(engine.h)
     if not p:

@@ -302,6 +302,20 @@ class Engine:
                                             int(node) | (2 if pred else 0) | (4 if common else 0)))
         return (out, cnt) if counters else out
 
+    def debug_walk_stats(self, table_id, src, dst, dport, proto):
+        """MEASUREMENT: per tuple, the loads a SINGLE launch on table_id makes of the table's
+        structure (pg_debug_walk_stats) -> (lds_reads u32[n], mem_reads u32[n], launch STAGE)"""
+        import numpy as np
+        n = len(src)
+        a = [np.ascontiguousarray(x, dt) for x, dt in ((src, np.uint32), (dst, np.uint32), (dport, np.uint16),
+                                                       (proto, np.uint8))]
+        p = lambda x: x.ctypes.data_as(C.c_void_p)
+        t = _capi.pg_tuple_soa(p(a[0]), p(a[1]), None, p(a[2]), p(a[3]))
+        nl, nm, st = np.zeros(n, np.uint32), np.zeros(n, np.uint32), C.c_int()
+        self._ck(lib.pg_debug_walk_stats(self.h, table_id, C.byref(t), n, nl.ctypes.data_as(C.POINTER(C.c_uint32)),
+                                         nm.ctypes.data_as(C.POINTER(C.c_uint32)), C.byref(st)))
+        return nl, nm, st.value
+
     def node_stats(self):
         """node classifier size {ip_classes, key_classes, image_bytes, cross_bytes}, or None."""
         a, b = C.c_uint32(), C.c_uint32()
