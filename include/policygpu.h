@@ -157,7 +157,11 @@ int pg_ctx_device(const pg_ctx* ctx);
  * rebuilt with level-compressed 12/16-bit trie strides and keep them when the result still
  * fits in LDS; default 4096, 0 = off; blobs too large for LDS are always level-compressed),
  * "lc_dense12" (boundaries a subtree needs for a 12-bit stride, default 16), "lc_max_stride"
- * (widest level-compressed stride: 12, 16 or 18, default 16), "lc_node" (1/0:
+ * (widest level-compressed stride: 12, 16 or 18, default 16), "lc_root_bits" (src-trie root
+ * stride cap of blobs read from HBM, whose root alone a launch stages in LDS: 4..14, default
+ * 12), "candi" (1/0: candidates inline in the 8-B trie entries of HBM-resident candidate tables
+ * no live rule of which tests dst, default 1), "fd" (1/0: fixed-depth form of dst-independent
+ * cross-product tables, default 1), "lc_node" (1/0:
  * level-compressed node tries, default 0), "node_common" (1/0: common-row section of node
  * images, default 1), "pair" (1/0: the PAIR structure -- src x dst classes, then x key classes
  * -- for tables the cross product cannot take, default 1; 0 = candidate lists; 2 = wherever it

@@ -83,10 +83,46 @@ def test_large_table_uses_candidate_mode():
     for k in range(20000):       # > 16384 rules, 20k src x 1k key classes: no product fits
         rules.append({"action": k % 2, "src": "10.%d.%d.0/24" % (k // 256, k % 256), "dst": "",
                       "udp": {"src": [0, 65535], "dst": [k % 1000, k % 1000 + 5]}})
-    e = engine_with({"big": rules})
-    assert e.table_stats(0)["structure"] == "cand"
     anchors = [(10 << 24) | (k << 8) for k in range(0, 20000, 37)]
     tup = fz.rand_tuples(np.random.default_rng(9), 30000, anchors)
+    # no rule tests dst: the inline-candidate form (CANDI); with it off, the record form
+    for candi, want in ((1, "candi"), (0, "cand")):
+        with tuning("candi", candi, 1):
+            e = engine_with({"big": rules})
+            assert e.table_stats(0)["structure"] == want
+        check(e, "big", rules, tup)
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_candi_nested_prefixes_and_defaults(seed):
+    """CANDI (dst-free candidate tables read from HBM): src classes with no candidate (the
+    table's default inline), one candidate (inline: key range, action, rule), and several
+    (nested /16 /24 /30 prefixes: the leaf points at the record list, whose last record carries
+    the last-record flag); unconditional rules ending lists; ANY-protocol packets (linear);
+    classes reached through root leaves (records)."""
+    rnd = random.Random(300 + seed)
+    rules = []
+    for k in range(18000):
+        a, b = rnd.randrange(6), rnd.randrange(64)
+        src = rnd.choice(["10.%d.0.0/16" % a, "10.%d.%d.0/24" % (a, b), "10.%d.%d.%d/30" % (a, b, 4 * rnd.randrange(64)),
+                          "10.%d.%d.%d/32" % (a, b, rnd.randrange(256)), "172.%d.0.0/12" % (16 + 16 * (k % 2))])
+        r = {"action": rnd.randrange(2), "src": src, "dst": ""}
+        kind = rnd.random()
+        if kind < 0.4:
+            lo = rnd.randrange(1, 60000)
+            r["tcp"] = {"src": [0, 65535], "dst": [lo, lo + rnd.choice([0, 3, 100])]}
+        elif kind < 0.8:
+            lo = rnd.randrange(1, 60000)
+            r["udp"] = {"src": [0, 65535], "dst": [lo, lo + rnd.choice([0, 3, 100])]}
+        rules.append(r)
+    if seed == 1:
+        rules.append({"action": 1, "src": "", "dst": ""})
+    with tuning("cross_max_rules", 0, 1 << 20), tuning("pair", 0, 1):  # (its cross product would fit)
+        e = engine_with({"big": rules})
+        assert e.table_stats(0)["structure"] == "candi"
+    anchors = [(10 << 24) | (a << 16) | (b << 8) for a in range(7) for b in range(0, 66, 3)] + \
+              [(172 << 24) | (k << 20) for k in range(4)]
+    tup = fz.rand_tuples(np.random.default_rng(400 + seed), 40000, anchors, any_pct=0.02)
     check(e, "big", rules, tup)
 
 

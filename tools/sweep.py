@@ -33,8 +33,11 @@ def main():
     ap.add_argument("--counters", action="store_true", help="classify with per-rule hit counters")
     ap.add_argument("--pre", action="append", default=[], help="key=v set before the tables are compiled")
     ap.add_argument("--ns", type=int, default=0, help="configs 3/5: namespaces (default 10)")
+    ap.add_argument("--rules", type=int, default=0, help="config 2: rules of the gen-policy-shaped table")
     a = ap.parse_args()
     kw = {"n_tuples": a.tuples} if a.tuples else {}
+    if a.rules:
+        kw["n_rules"] = a.rules
     if a.ns:
         kw["n_ns"] = a.ns
     for t in a.pre:
@@ -80,7 +83,7 @@ def main():
     for i, combo in enumerate(combos):
         ms = float(np.median(times[i]))
         extra = {"blob": e.table_stats(w.table_id)} if w.mode == 0 and i == 0 else {}
-        print(json.dumps({"lib": name, "config": a.config, "counters": a.counters, "pre": a.pre, "ns": a.ns, **dict(zip(keys, combo)), "ms": round(ms, 4),
+        print(json.dumps({"lib": name, "config": a.config, "counters": a.counters, "pre": a.pre, "ns": a.ns, "rules": a.rules, **dict(zip(keys, combo)), "ms": round(ms, 4),
                           "gpps": round(n / ms / 1e6, 1), "GBps": round(n * bpt / ms / 1e6, 1),
                           "same_output": bool(torch.equal(outs[i], ref)), **extra}), flush=True)
 

@@ -27,6 +27,16 @@ constexpr uint32_t kFlagFD = 32u;
 // no rule of the table tests dst (set by engine.cpp in DevTable::fsk, not in the blob): SINGLE
 // launches do not read the dst stream
 constexpr uint32_t kFlagDstFree = 64u;
+// CANDI ("candidates inline", fastpath.cpp build_candi): a CAND table no live rule of which
+// tests dst, read from HBM. Below the (LDS-staged, 4-B) src root, trie entries are 8 B and a
+// leaf carries its src class's single candidate (or the table's default) itself, so most
+// lookups end with the trie read instead of a further record gather (blobwalk candi_walk).
+constexpr uint32_t kFlagCandI = 128u;
+// 8-B CANDI entry {w0, w1}: w1 bit 31 clear = an inline candidate: key range klo = w0 & 0x3FFFF,
+// khi = w0 >> 18 | (w1 & 15) << 14, action (w1 >> 4) & 3, rule w1 >> 6 (relative to the table's
+// first rule; kCandiDefault = the table's default verdict); w1 bit 31 set = kCandiInternal:
+// child block at word w0, stride w1 & 31; else the class's record list at record w0.
+constexpr uint32_t kCandiNode = 1u << 31, kCandiInternal = 1u << 30, kCandiDefault = 0x1FFFFFFu;
 constexpr uint32_t kPairHdr = 12u;  // PAIR blob header words: dst root, d1, pair table, n_dst_classes
 constexpr uint32_t kLeaf = 0x80000000u;
 // non-leaf trie entry: child block offset (words) | child stride << kTrieStrideShift
@@ -71,6 +81,7 @@ struct BlobTab {
     uint32_t kroot;  // key trie root (words)
     uint32_t xoff;   // cross table (CROSS) or first record (CAND), words
     uint32_t nkc;    // key classes
+    uint32_t rbase;  // first rule's counter slot (CANDI inline candidates)
 };
 
 // Record (16 B): {dnet, klo | dlen << 18 | last << 24, khi, verdict}: matches when the dst
@@ -96,11 +107,65 @@ template <bool PRED = false, class L, class L0, int Q>
 PG_HD void blob_walk(const L (&ld)[Q], const L0 (&ld0)[Q], const BlobTab (&tb)[Q], const bool (&on)[Q],
                      const uint32_t (&src)[Q], const uint32_t (&dst)[Q], const uint32_t (&key)[Q], uint32_t (&w)[Q]) {
     uint32_t es[Q], ek[Q], ss[Q], sk[Q], ed[Q], sd[Q];
+    // CANDI lanes (blobwalk.hpp kFlagCandI): 8-B entries below the root, inline candidates
+    uint32_t cw[Q], cst[Q], pos[Q];
+    bool ci[Q], cwalk[Q], pend[Q], anyci = false;
+    PG_UNROLL
+    for (int j = 0; j < Q; j++) {
+        ci[j] = on[j] && (tb[j].fsk & kFlagCandI);
+        anyci |= ci[j];
+        cwalk[j] = pend[j] = false;
+        pos[j] = cw[j] = cst[j] = 0;
+    }
+    if (anyci) {
+        PG_UNROLL
+        for (int j = 0; j < Q; j++) {
+            if (!ci[j]) continue;
+            ss[j] = 32u - ((tb[j].fsk >> 8) & 0xFFu);
+            const uint32_t e = ld0[j].u32(kSrcRoot + (src[j] >> ss[j]));
+            if (e & kLeaf) {
+                pos[j] = tb[j].xoff + 4u * (e & ~kLeaf);
+                pend[j] = true;
+            } else {
+                cw[j] = trie_child(e);
+                cst[j] = trie_stride(e);
+                cwalk[j] = true;
+            }
+        }
+        for (;;) {
+            bool more = false;
+            PG_UNROLL
+            for (int j = 0; j < Q; j++) more |= cwalk[j];
+            if (!more) break;
+            PG_UNROLL
+            for (int j = 0; j < Q; j++) {
+                if (!cwalk[j]) continue;
+                ss[j] -= cst[j];
+                const W2 v = ld[j].u2(cw[j] + 2u * ((src[j] >> ss[j]) & ((1u << cst[j]) - 1u)));
+                if (v.y & kCandiNode) {
+                    if (v.y & kCandiInternal) {
+                        cw[j] = v.x;
+                        cst[j] = v.y & 31u;
+                    } else {
+                        pos[j] = tb[j].xoff + 4u * v.x;
+                        pend[j] = true;
+                        cwalk[j] = false;
+                    }
+                } else {
+                    const uint32_t klo = v.x & 0x3FFFFu, khi = (v.x >> 18) | ((v.y & 15u) << 14);
+                    const uint32_t rel = (v.y >> 6) & kCandiDefault;
+                    const bool hit = key[j] >= klo && key[j] <= khi && rel != kCandiDefault;
+                    w[j] = hit ? (((v.y >> 4) & 3u) << 30) | (tb[j].rbase + rel) : tb[j].dflt;
+                    cwalk[j] = false;
+                }
+            }
+        }
+    }
     PG_UNROLL
     for (int j = 0; j < Q; j++) {
         es[j] = ek[j] = ed[j] = kLeaf;
         ss[j] = sk[j] = sd[j] = 0;
-        if (on[j]) {
+        if (on[j] && !ci[j]) {
             ss[j] = 32u - ((tb[j].fsk >> 8) & 0xFFu);
             es[j] = ld0[j].u32(kSrcRoot + (src[j] >> ss[j]));
             if (tb[j].fsk & (kFlagCross | kFlagPair)) {
@@ -112,7 +177,7 @@ PG_HD void blob_walk(const L (&ld)[Q], const L0 (&ld0)[Q], const BlobTab (&tb)[Q
     // PAIR tables: the dst trie too (its root and stride are in the blob header)
     PG_UNROLL
     for (int j = 0; j < Q; j++) {
-        if (on[j] && (tb[j].fsk & kFlagPair)) {
+        if (on[j] && !ci[j] && (tb[j].fsk & kFlagPair)) {
             const W2 h = ld[j].u2(kPairHdr);
             sd[j] = 32u - h.y;
             ed[j] = ld[j].u32(h.x + (dst[j] >> sd[j]));
@@ -156,14 +221,10 @@ PG_HD void blob_walk(const L (&ld)[Q], const L0 (&ld0)[Q], const BlobTab (&tb)[Q
             }
         }
     }
-    // cross entry, or the first record of the src class's candidate list
-    uint32_t pos[Q];
-    bool pend[Q];
+    // cross entry, or the first record of the src class's candidate list (CANDI lanes: set above)
     PG_UNROLL
     for (int j = 0; j < Q; j++) {
-        pend[j] = false;
-        pos[j] = 0;
-        if (!on[j]) continue;
+        if (!on[j] || ci[j]) continue;
         const uint32_t sc = es[j] & ~kLeaf;
         if (tb[j].fsk & kFlagPair) {  // (src, dst) -> pair class -> x key class -> verdict
             const W2 h = ld[j].u2(kPairHdr + 2u);

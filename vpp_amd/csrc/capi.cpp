@@ -488,7 +488,7 @@ int pg_debug_walk_blob(pg_ctx* ctx, const char* acl_name, const uint32_t* src, c
     BlobTab tb[Q];
     for (int j = 0; j < Q; j++) {
         ld[j] = HostLoader{E.host.blobs.data() + hd.blob_off};
-        tb[j] = BlobTab{hd.fsk, hd.dflt, hd.kroot, hd.xoff, hd.nkc};
+        tb[j] = BlobTab{hd.fsk, hd.dflt, hd.kroot, hd.xoff, hd.nkc, hd.rule_base};
     }
     for (uint64_t i0 = 0; i0 < n; i0 += Q) {
         bool on[Q];
@@ -585,7 +585,7 @@ int pg_debug_walk_stats(pg_ctx* ctx, int table_id, const pg_tuple_soa* t, uint64
             } else {
                 const CountingLoader ld[1] = {whole};
                 const CountingLoader ld0[1] = {CountingLoader{blob, st != 0, &nl, &nm}};
-                const BlobTab tb[1] = {BlobTab{hd.fsk, hd.dflt, hd.kroot, hd.xoff, hd.nkc}};
+                const BlobTab tb[1] = {BlobTab{hd.fsk, hd.dflt, hd.kroot, hd.xoff, hd.nkc, hd.rule_base}};
                 const bool on[1] = {true};
                 const uint32_t s1[1] = {s}, d1[1] = {d}, k1[1] = {key};
                 uint32_t w1[1];

@@ -118,7 +118,7 @@ PG_HD void eval_q(const DevTableSet& T, const uint32_t* blobs, const DevTable (&
     for (int j = 0; j < Q; j++) {
         ld[j] = DevLoader{blobs + tab[j].blob_off};
         ld0[j] = rootb ? DevLoader{rootb} : ld[j];
-        tb[j] = BlobTab{tab[j].fsk, tab[j].dflt, tab[j].kroot, tab[j].xoff, tab[j].nkc};
+        tb[j] = BlobTab{tab[j].fsk, tab[j].dflt, tab[j].kroot, tab[j].xoff, tab[j].nkc, tab[j].rule_base};
         fd[j] = act[j] && (tab[j].fsk & kFlagFD);
         on[j] = act[j] && !fd[j] && !(tab[j].fsk & kFlagLinear);
         anyfd |= fd[j];
@@ -154,7 +154,7 @@ PG_NOINLINE uint32_t eval_one(const DevRule* rules, const uint32_t* blobs, const
         if (key < kWalkKeyLimit) return w1[0];
     } else if (!(tab.fsk & kFlagLinear) && key < kWalkKeyLimit) {
         const DevLoader ld[1] = {DevLoader{blobs + tab.blob_off}};
-        const BlobTab tb[1] = {BlobTab{tab.fsk, tab.dflt, tab.kroot, tab.xoff, tab.nkc}};
+        const BlobTab tb[1] = {BlobTab{tab.fsk, tab.dflt, tab.kroot, tab.xoff, tab.nkc, tab.rule_base}};
         const bool on[1] = {true};
         const uint32_t s1[1] = {src}, d1[1] = {dst}, k1[1] = {key};
         uint32_t w1[1];

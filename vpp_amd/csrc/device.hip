@@ -333,8 +333,9 @@ __device__ __forceinline__ void stream_store(V v, V* p) {
 // Stream pipelining (PG_PREFETCH): 1 = the next group's loads are issued at the top of each
 // iteration; 2 = (NODE) issued right after the first cross-entry gather of the iteration, so
 // waiting for that gather does not also wait for them (vmcnt retires in issue order); 0 = none;
-// -1 (default) = per mode: none for SINGLE (all lookups in LDS, occupancy hides the stream),
-// top-of-iteration for PERPOD / CONN (tools/sweep.py A/B on MI355X).
+// -1 (default) = per mode: none for SINGLE over an LDS-staged blob (all lookups in LDS,
+// occupancy hides the stream), top-of-iteration for SINGLE over a blob in HBM and for PERPOD /
+// CONN (tools/sweep.py A/B on MI355X).
 #ifndef PG_PREFETCH
 #define PG_PREFETCH -1
 #endif
@@ -345,14 +346,14 @@ __device__ __forceinline__ void stream_store(V v, V* p) {
 #define PG_PRED 0
 #endif
 // tuples of a group classified together (lockstep chunk), per mode, each dividing PG_TPL
-// SINGLE: blob staged in LDS (STAGE 1) one tuple at a time, blob in HBM two (A/B on MI355X:
-// config 2 331 / 343 / 348 Gpps at 4 / 2 / 1, with counters 307 / 316 / 325; config 4 119 /
-// 121.5 / 113.5)
+// SINGLE: blob staged in LDS (STAGE 1) one tuple at a time (A/B on MI355X: config 2 331 / 343 /
+// 348 Gpps at 4 / 2 / 1, with counters 307 / 316 / 325), blob in HBM four (config 4 with the
+// inline-candidate form and a 12-bit staged root: 169.3 / 163.5 / 124 at 4 / 2 / 1)
 #ifndef PG_QSINGLE_LDS
 #define PG_QSINGLE_LDS 1
 #endif
 #ifndef PG_QSINGLE
-#define PG_QSINGLE 2
+#define PG_QSINGLE 4
 #endif
 #ifndef PG_QPOD  // PERPOD: 2 (A/B on MI355X, config 3: 237 vs 198 Gpps at 4 -- fewer registers)
 #define PG_QPOD 2
@@ -480,7 +481,11 @@ void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
     };
     uint64_t q = first;
     Group cur;
-    constexpr int PF = FD ? PG_PREFETCH_FD : (PG_PREFETCH >= 0 ? PG_PREFETCH : (MODE == 0 ? 0 : 1));
+    // default: SINGLE over an LDS-staged blob none, SINGLE over a blob in HBM (STAGE 0 / 2) and
+    // the node modes the next group at the top of the iteration (A/B on MI355X, config 4 with
+    // four tuples per chunk: 172.9 vs 169.3 Gpps)
+    constexpr int PF = FD ? PG_PREFETCH_FD
+                          : (PG_PREFETCH >= 0 ? PG_PREFETCH : (MODE == 0 && STAGE != 0 && STAGE != 2 ? 0 : 1));
     if (PF && q < nfull) cur = load(q);
     while (q < nfull) {
         const uint64_t qn = q + stride;
@@ -771,9 +776,9 @@ static void launch_one(const DevTableSet& T, const Tuning& tu, int t, const uint
                        unsigned long long* counters, hipStream_t st, size_t hist, uint32_t stage, uint64_t items) {
     if constexpr (STAGE) {
         // 512 (A/B on MI355X: SINGLE with counters +14 % over 1024 at config 2; without
-        // counters +2.5 % since SINGLE classifies one tuple per chunk, v15), except SINGLE
-        // without counters over an HBM blob with its root staged: 1024 (config 4 +1.3 %)
-        const uint32_t bs = tu.block_stage ? tu.block_stage : (MODE == 0 && !COUNT && (STAGE & 7) == 2 ? 1024u : 512u);
+        // counters +2.5 % since SINGLE classifies one tuple per chunk, v15; config 4 over its
+        // 12-bit staged root 163 vs 132 Gpps at 1024)
+        const uint32_t bs = tu.block_stage ? tu.block_stage : 512u;
         if (bs == 1024u)
             return launch_bs<MODE, COUNT, VEC, STAGE, NODE, 1024>(T, tu, t, src, dst, sport, dport, proto, n, out,
                                                                   counters, st, hist, stage, items);

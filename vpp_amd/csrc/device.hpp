@@ -131,12 +131,14 @@ struct Tuning {
     uint32_t lc_lds = 4096;        // LC rebuild of LDS-sized blobs of at least this many words (0 = off)
     uint32_t lc_dense12 = 16;      // boundaries in a child's span that earn it a 12-bit stride
     uint32_t lc_max_stride = 16;   // widest level-compressed stride (12, 16, 18)
+    uint32_t lc_root_bits = 12;    // src-trie root stride cap of HBM-resident (level-compressed) blobs
     uint32_t pair = 1;             // PAIR for tables CROSS cannot take (0 = CAND, 2 = wherever it fits)
     uint32_t node_build = 1;       // build the node classifier (PERPOD / CONN)
     uint32_t node_root_bits = 12;  // its IPv4 / key trie root stride cap (4..16)
     uint32_t lc_node = 0;          // level-compressed node IPv4 trie
     uint32_t node_common = 1;      // common-row section of node images
     uint32_t fd = 1;               // FD form of dst-independent CROSS tables that fit LDS
+    uint32_t candi = 1;            // CANDI form (inline candidates) of dst-independent HBM-resident CAND tables
     uint32_t cross_max_rules = 1u << 20;  // CROSS (cross product) considered up to this many rules (within budget)
     // launches
     uint32_t blocks_per_cu = 0;    // cap on resident workgroups per CU (0 = occupancy)

@@ -29,12 +29,14 @@ const Knob kKnobs[] = {
     {"lc_lds", &Tuning::lc_lds, 0, 1 << 30, true},
     {"lc_dense12", &Tuning::lc_dense12, 1, 1 << 30, true},
     {"lc_max_stride", &Tuning::lc_max_stride, 12, 18, true},
+    {"lc_root_bits", &Tuning::lc_root_bits, 4, 14, true},
     {"pair", &Tuning::pair, 0, 2, true},
     {"node_build", &Tuning::node_build, 0, 1, true},
     {"node_root_bits", &Tuning::node_root_bits, 4, 16, true},
     {"lc_node", &Tuning::lc_node, 0, 1, true},
     {"node_common", &Tuning::node_common, 0, 1, true},
     {"fd", &Tuning::fd, 0, 1, true},
+    {"candi", &Tuning::candi, 0, 1, true},
     {"cross_max_rules", &Tuning::cross_max_rules, 0, 1 << 24, true},
     {"blocks_per_cu", &Tuning::blocks_per_cu, 0, 64, false},
     {"stage_max_words", &Tuning::stage_max_words, 0, 36864, false},

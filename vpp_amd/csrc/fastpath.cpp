@@ -45,8 +45,6 @@ namespace pg {
 
 namespace {
 
-constexpr uint32_t kLeaf = 0x80000000u;
-
 struct VecHash {
     size_t operator()(const std::vector<uint32_t>& v) const {
         uint64_t h = 1469598103934665603ull;
@@ -71,7 +69,9 @@ constexpr uint32_t kTrieFail = 0xFFFFFFFFu;
 // Tuning::lc_dense12: boundaries in a child's span that earn it a 12-bit stride;
 // Tuning::lc_max_stride: widest stride level compression may pick (A/B on MI355X, config 4:
 // 16 = +4 % over 18, 12 = -3 %)
-constexpr uint32_t kLcRootBits = 14;  // HBM-resident blobs: the root alone is staged in LDS (64 KiB)
+// HBM-resident blobs: the root alone is staged in LDS, its stride capped by Tuning::lc_root_bits
+// (default 12: 16 KiB per workgroup; A/B on MI355X, config 4: 163 Gpps at 12 vs 131 at 14 --
+// the 64 KiB root of 14 bits held the launch to half the resident waves)
 // enc: kEncBlob (blobwalk.hpp trie_child / trie_stride); kEncNode, the node image's encoding
 // (blobwalk.hpp node_child): a non-leaf entry holds the child's BYTE offset << 10 | stride << 5
 // | the address shift of the child level, so a step is one bit-field extract and one shifted
@@ -428,7 +428,7 @@ bool build_fast_table(const DevRule* rules, uint32_t n, uint32_t rule_base, uint
                                 break;
                             }
                     }
-                const uint32_t s1 = std::min<uint32_t>(pick_stride(sb.size(), 32, tu), lc ? kLcRootBits : 32u);
+                const uint32_t s1 = std::min<uint32_t>(pick_stride(sb.size(), 32, tu), lc ? tu.lc_root_bits : 32u);
                 if (build_trie(blob, sb, sint_cls, 32, s1, tu, lc) != kSrcRoot) return false;
                 const uint32_t k1 = pick_stride(kb.size(), 18, tu);
                 const uint32_t kroot = build_trie(blob, kb, kseg_cls, 18, k1, tu, lc);
@@ -486,7 +486,7 @@ bool build_fast_table(const DevRule* rules, uint32_t n, uint32_t rule_base, uint
     }
     if (cross) {
         const uint32_t nkc = (uint32_t)key_sets.size();
-        const uint32_t s1 = std::min<uint32_t>(pick_stride(sb.size(), 32, tu), lc ? kLcRootBits : 32u);
+        const uint32_t s1 = std::min<uint32_t>(pick_stride(sb.size(), 32, tu), lc ? tu.lc_root_bits : 32u);
         if (build_trie(blob, sb, sint_cls, 32, s1, tu, lc) != kSrcRoot) return false;
         blob[2] = kSrcRoot;
         blob[3] = s1;
@@ -539,6 +539,115 @@ bool build_fast_table(const DevRule* rules, uint32_t n, uint32_t rule_base, uint
     if (!cross && tu.pair && n <= kPairMaxRules && try_pair()) return true;
     blob_header_only();
 
+    // ---- CANDI: a candidate table read from HBM whose live rules test no dst ------------------
+    // Below the 4-B src root (staged in LDS by the launch) every trie entry is 8 B (blobwalk.hpp
+    // candi_walk): an internal entry, a leaf whose src class has at most one candidate carrying
+    // that candidate (key range, action, rule) -- or the table's default -- itself, or a leaf
+    // pointing at the class's record list (classes of two or more candidates). A lookup then
+    // ends with its last trie read instead of a further record gather; on MI355X a gather costs
+    // the same for 4 and 16 B, per active lane (tools/gather_probe.hip), so one gather less per
+    // tuple is the lever for tables over LDS. Root leaves keep the record form.
+    bool cand_dst_free = true;
+    for (uint32_t i = 0; i < n; i++) cand_dst_free &= !live(rules[i]) || rules[i].dmask == 0;
+    if (lc && tu.candi && cand_dst_free && n < kCandiDefault) {
+        std::vector<uint32_t> tmp;  // the 4-B trie (kEncBlob, leaf = kLeaf | src class)
+        const uint32_t s1 = std::min<uint32_t>(pick_stride(sb.size(), 32, tu), tu.lc_root_bits);
+        if (build_trie(tmp, sb, sint_cls, 32, s1, tu, lc) == 0) {
+            std::vector<int64_t> rec_of(nsc, -1);  // record list index of a class (root leaves, pointers)
+            std::vector<uint32_t> rec_cls;
+            auto rec = [&](uint32_t c) {
+                if (rec_of[c] < 0) rec_of[c] = (int64_t)rec_cls.size(), rec_cls.push_back(c);
+                return (uint32_t)rec_of[c];
+            };
+            // blocks: (old offset, stride) -> new word offset; breadth-first from the root
+            blob.resize(kSrcRoot + (1u << s1), 0);
+            struct Blk {
+                uint32_t old_off, stride, new_off;
+            };
+            std::vector<Blk> q{{0, s1, kSrcRoot}};
+            bool ok = true;
+            std::vector<uint32_t> rec_at;  // record index per referenced class, assigned below
+            for (size_t qi = 0; qi < q.size() && ok; qi++) {
+                const Blk b = q[qi];
+                for (uint32_t e = 0; e < (1u << b.stride) && ok; e++) {
+                    const uint32_t x = tmp[b.old_off + e];
+                    uint32_t w0 = 0, w1 = 0;
+                    if (!(x & kLeaf)) {  // internal: allocate the child's 8-B block
+                        const uint32_t st = trie_stride(x);
+                        const uint64_t child = blob.size();
+                        if (child + (2ull << st) > kTrieChildMask) {
+                            ok = false;
+                            break;
+                        }
+                        blob.resize(blob.size() + (2u << st), 0);
+                        q.push_back({trie_child(x), st, (uint32_t)child});
+                        w0 = (uint32_t)child;
+                        w1 = kCandiNode | kCandiInternal | st;
+                        if (qi == 0) {  // root entries stay 4 B
+                            blob[b.new_off + e] = (uint32_t)child | (st << kTrieStrideShift);
+                            continue;
+                        }
+                    } else {
+                        const uint32_t c = x & ~kLeaf;
+                        const std::vector<uint32_t>& L = src_lists[c];
+                        if (qi == 0) {
+                            blob[b.new_off + e] = kLeaf | rec(c);
+                            continue;
+                        }
+                        if (L.size() >= 2) {
+                            w0 = rec(c);
+                            w1 = kCandiNode;
+                        } else if (L.empty()) {
+                            w0 = 0 | (kRecKeyAll & 0x3FFFu) << 18;
+                            w1 = (kRecKeyAll >> 14) | kCandiDefault << 6;
+                        } else {
+                            const DevRule& R = rules[L[0]];
+                            w0 = R.klo | (R.khi & 0x3FFFu) << 18;
+                            w1 = (R.khi >> 14) | (R.act & 3u) << 4 | L[0] << 6;
+                        }
+                    }
+                    blob[b.new_off + 2 * e] = w0;
+                    blob[b.new_off + 2 * e + 1] = w1;
+                }
+            }
+            if (ok) {
+                blob[0] = kFlagCandI;
+                blob[2] = kSrcRoot;
+                blob[3] = s1;
+                while (blob.size() % 4) blob.push_back(0);
+                blob[6] = (uint32_t)blob.size();
+                // record lists of the referenced classes, in reference order; rec(c) numbered the
+                // lists, so list k starts at record first[k]
+                std::vector<uint32_t> first(rec_cls.size());
+                uint64_t nrec = 0;
+                for (size_t k = 0; k < rec_cls.size(); k++) {
+                    first[k] = (uint32_t)nrec;
+                    nrec += std::max<size_t>(src_lists[rec_cls[k]].size(), 1);
+                }
+                if (nrec < (1ull << 29)) {
+                    // leaves and pointers hold list numbers: turn them into record indices
+                    for (uint32_t e = 0; e < (1u << s1); e++)
+                        if (blob[kSrcRoot + e] & kLeaf) blob[kSrcRoot + e] = kLeaf | first[blob[kSrcRoot + e] & ~kLeaf];
+                    for (size_t qi = 1; qi < q.size(); qi++)
+                        for (uint32_t e = 0; e < (1u << q[qi].stride); e++) {
+                            uint32_t* v = &blob[q[qi].new_off + 2 * e];
+                            if ((v[1] & kCandiNode) && !(v[1] & kCandiInternal)) v[0] = first[v[0]];
+                        }
+                    for (uint32_t c : rec_cls) {
+                        const std::vector<uint32_t>& L = src_lists[c];
+                        for (size_t i = 0; i < L.size(); i++) {
+                            const uint32_t r = L[i];
+                            put_rec(0, i + 1 == L.size() ? kRecLast >> 18 : 0u, rules[r].klo, rules[r].khi, verdict(r));
+                        }
+                        if (L.empty()) put_rec(0, 0, 0, kRecKeyAll, dflt);
+                    }
+                    return true;
+                }
+            }
+        }
+        blob_header_only();
+    }
+
     // ---- candidate mode: src trie leaves point at the class's record list -------------------
     std::vector<uint32_t> first_rec(nsc);
     uint64_t nrec = 0;
@@ -549,7 +658,7 @@ bool build_fast_table(const DevRule* rules, uint32_t n, uint32_t rule_base, uint
     if (nrec >= (1ull << 29)) return false;
     std::vector<uint32_t> leaf(sb.size());
     for (size_t k = 0; k < sb.size(); k++) leaf[k] = first_rec[sint_cls[k]];
-    const uint32_t s1 = std::min<uint32_t>(pick_stride(sb.size(), 32, tu), lc ? kLcRootBits : 32u);
+    const uint32_t s1 = std::min<uint32_t>(pick_stride(sb.size(), 32, tu), lc ? tu.lc_root_bits : 32u);
     if (build_trie(blob, sb, leaf, 32, s1, tu, lc) != kSrcRoot) return false;
     blob[0] = kFlagCand;
     blob[2] = kSrcRoot;

@@ -268,8 +268,8 @@ class Engine:
         v = [C.c_uint32() for _ in range(4)]
         self._ck(lib.pg_table_stats(self.h, tid, *[C.byref(x) for x in v]))
         f, nbytes, nsc, nkc = (x.value for x in v)
-        mode = "linear" if f & 8 else ("fd" if f & 32 else ("pair" if f & 16 else ("cand" if f & 4 else (
-            "cross+lists" if f & 2 else "cross"))))
+        mode = "linear" if f & 8 else ("fd" if f & 32 else ("pair" if f & 16 else ("candi" if f & 128 else (
+            "cand" if f & 4 else ("cross+lists" if f & 2 else "cross")))))
         return {"structure": mode, "blob_bytes": nbytes, "src_classes": nsc, "key_classes": nkc,
                 "dst_free": bool(f & 64)}
 
