@@ -1,37 +1,9 @@
-#!/bin/bash
-# FD kernel (STAGE 4) first look: GPU tests, cold-start transient, driver bench, A/B of chunk /
-# prefetch builds and workgroup sizes (tools/sweep.py, one process per build).
+# FD tables read from HBM (STAGE 5): lockstep chunk 1 / 2 / 4, prefetch; config 4 at the new defaults
 set -o pipefail
-TAG=${1:-abfd}
-R=$(pwd)
-O=$R/gpurun_out/$TAG
-mkdir -p "$O"
-step() { echo "[$(date +%T)] $*"; }
-step tests
-timeout -k 10 600 python -u -m pytest tests/test_gpu_configs.py tests/test_gpu_parity.py -m gpu -x -q --timeout 300 \
-    --timeout-method thread > "$O/gpu_tests.log" 2>&1 || { tail -30 "$O/gpu_tests.log"; exit 1; }
-tail -2 "$O/gpu_tests.log"
-step bench driver command
-timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 > "$O/bench_drv.json" 2> "$O/bench_drv.err" \
-    || { tail -20 "$O/bench_drv.err"; exit 1; }
-cat "$O/bench_drv.json"
-step ramp
-timeout -k 10 180 python tools/ramp_probe.py --config 2 > "$O/ramp.json" 2> "$O/ramp.err" || { tail -20 "$O/ramp.err"; exit 1; }
-python -c "
-import json
-for l in open('$O/ramp.json'):
-    d=json.loads(l); print(d['phase'], d['summary_us'], d['us'][:30:3])
-"
-for r in 1 2; do
-for lib in libpolicygpu.so libpolicygpu_qfd2.so libpolicygpu_qfd4.so libpolicygpu_pf1.so; do
-    step sweep $lib
-    VPP_AMD_LIB=$R/vpp_amd/$lib timeout -k 10 200 python tools/sweep.py --config 2 --rounds 3 --reps 10 \
-        --tune block_stage=256,512,1024 >> "$O/sweep.jsonl" 2> "$O/sweep.err" || { tail -20 "$O/sweep.err"; exit 1; }
+O=gpurun_out/abfd5; mkdir -p $O
+run() { VPP_AMD_LIB=$PWD/vpp_amd/$1 timeout -k 10 250 python tools/sweep.py --rounds 2 --reps 10 "${@:2}" | sed "s/^/$1 /" | tee -a $O/sweep.log; }
+run libpolicygpu.so --config 4 || exit 1
+for lib in libpolicygpu.so libpolicygpu_fdq1.so libpolicygpu_fdq4.so libpolicygpu_fdpf.so; do
+  run $lib --config 2 --rules 100000 || exit 1
+  run $lib --config 7 || exit 1
 done
-done
-python -c "
-import json
-for l in open('$O/sweep.jsonl'):
-    d=json.loads(l); print(d['lib'], d.get('block_stage'), d['ms'], d['gpps'], d['same_output'])
-"
-step done

@@ -22,6 +22,8 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <utility>
 
@@ -753,9 +755,13 @@ static int grid_resident(K kernel, int bs, size_t lds, uint64_t items, uint32_t 
     int per_cu = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, bs, lds) != hipSuccess || per_cu < 1)
         per_cu = 1;
+    const int occ = per_cu;
     if (blocks_per_cu) per_cu = std::min<int>(per_cu, (int)blocks_per_cu);
     const uint64_t g = (items + bs - 1) / bs;
-    return (int)std::max<uint64_t>(1, std::min<uint64_t>(g, (uint64_t)num_cus() * per_cu));
+    const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>(g, (uint64_t)num_cus() * per_cu));
+    static const bool dbg = std::getenv("PG_DEBUG_LAUNCH") != nullptr;  // measurement aid: launch geometry
+    if (dbg) std::fprintf(stderr, "pg launch: block %d, LDS %zu B, occupancy %d blocks/CU, grid %d\n", bs, lds, occ, grid);
+    return grid;
 }
 
 template <int MODE, bool COUNT, bool VEC, int STAGE, bool NODE, int BS>
