@@ -321,3 +321,27 @@ def test_full_gen_policy_through_configurator():
     act, slot, _ = _expected_single(w, src, dst, dport, proto)
     assert np.array_equal(got[:k] >> 30, act) and np.array_equal(got[:k] & 0x3FFFFFFF, slot)
     assert len(np.unique(act)) == 2
+
+
+@pytest.mark.parametrize("fields", [0, 1, 2, 3])
+def test_stream_probe_reads_the_fields_it_is_told_to(fields):
+    """pg_stream_probe (bench.py's stream ceiling): out = src ^ dport ^ proto (^ dst when
+    fields & 1, ^ sport when fields & 2) over a ragged batch (vector groups + remainder)."""
+    e, _ = _small_engine(3)
+    n = (1 << 20) + 13
+    rng = np.random.default_rng(fields)
+    src = rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32)
+    dst = rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32)
+    sport = rng.integers(0, 1 << 16, n).astype(np.uint16)
+    dport = rng.integers(0, 1 << 16, n).astype(np.uint16)
+    proto = rng.integers(0, 4, n).astype(np.uint8)
+    b = D.TupleBatch.from_numpy(src, dst, sport, dport, proto)
+    out = torch.empty(n, dtype=torch.int32, device="cuda")
+    D.stream_probe(e, fields, b, out)
+    torch.cuda.synchronize()
+    exp = src ^ dport.astype(np.uint32) ^ proto.astype(np.uint32)
+    if fields & 1:
+        exp ^= dst
+    if fields & 2:
+        exp ^= sport.astype(np.uint32)
+    assert np.array_equal(out.cpu().numpy().view(np.uint32), exp)

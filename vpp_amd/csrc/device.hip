@@ -410,10 +410,21 @@ __device__ __forceinline__ void st_words(const Words<NW>& v, uint32_t* p) {
 #ifndef PG_NODE_WPE  // node kernels: minimum waves per SIMD the register allocation must allow (1 = any)
 #define PG_NODE_WPE 1
 #endif
+// CONN with hit counters (config 5): image + counter histogram (79 KB) leave LDS for two
+// workgroups per CU; 1024-thread workgroups, registers held to 64 (8 waves per SIMD) and no
+// stream prefetch (its 13 registers) put 32 waves per CU instead of 16 (A/B on MI355X,
+// gpurun_out/abocc: 89.1 -> 103.4 Gpps; the same 64-register cap on PERPOD spills and loses)
+#ifndef PG_CONN_COUNT_WPE
+#define PG_CONN_COUNT_WPE 8
+#endif
+template <int MODE, bool COUNT, bool NODE>
+constexpr int kernel_wpe() {
+    return !NODE ? 1 : (MODE == 2 && COUNT ? PG_CONN_COUNT_WPE : PG_NODE_WPE);
+}
 // STAGE_ + 8 (SINGLE, STAGE 0-2): the table is dst-free (kFlagDstFree: no rule tests dst), so
 // the dst stream is not read
 template <int MODE, bool COUNT, bool VEC, int STAGE_, bool NODE, int BS>
-__global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(NODE ? PG_NODE_WPE : 1)))
+__global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(kernel_wpe<MODE, COUNT, NODE>())))
 void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
                                                      const uint32_t* __restrict__ dst,
                                                      const uint16_t* __restrict__ sport,
@@ -487,7 +498,10 @@ void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
     // the node modes the next group at the top of the iteration (A/B on MI355X, config 4 with
     // four tuples per chunk: 172.9 vs 169.3 Gpps)
     constexpr int PF = FD ? PG_PREFETCH_FD
-                          : (PG_PREFETCH >= 0 ? PG_PREFETCH : (MODE == 0 && STAGE != 0 && STAGE != 2 ? 0 : 1));
+                          : (PG_PREFETCH >= 0 ? PG_PREFETCH
+                                              : ((MODE == 0 && STAGE != 0 && STAGE != 2) ||
+                                                 (NODE && MODE == 2 && COUNT && kernel_wpe<MODE, COUNT, NODE>() >= 8)
+                                                     ? 0 : 1));
     if (PF && q < nfull) cur = load(q);
     while (q < nfull) {
         const uint64_t qn = q + stride;
@@ -589,8 +603,8 @@ __global__ __launch_bounds__(BS) void k_stream_probe(const uint32_t* __restrict_
         Words<P> o;
 #pragma unroll
         for (int j = 0; j < P; j++)
-            o.w[j] = s.w[j] ^ d.w[j] ^ (dp.w[j / 2] >> (16 * (j & 1))) ^ (sp.w[j / 2] >> (16 * (j & 1))) ^
-                     (pr.w[j / 4] >> (8 * (j & 3)));
+            o.w[j] = s.w[j] ^ d.w[j] ^ ((dp.w[j / 2] >> (16 * (j & 1))) & 0xFFFFu) ^
+                     ((sp.w[j / 2] >> (16 * (j & 1))) & 0xFFFFu) ^ ((pr.w[j / 4] >> (8 * (j & 3))) & 0xFFu);
         st_words<P>(o, out + i0);
     }
     for (uint64_t i = nfull * P + first; i < n; i += stride)
@@ -784,7 +798,9 @@ static void launch_one(const DevTableSet& T, const Tuning& tu, int t, const uint
         // 512 (A/B on MI355X: SINGLE with counters +14 % over 1024 at config 2; without
         // counters +2.5 % since SINGLE classifies one tuple per chunk, v15; config 4 over its
         // 12-bit staged root 163 vs 132 Gpps at 1024)
-        const uint32_t bs = tu.block_stage ? tu.block_stage : 512u;
+        const uint32_t bs = tu.block_stage ? tu.block_stage
+                                           : (NODE && MODE == 2 && COUNT && kernel_wpe<MODE, COUNT, NODE>() >= 8 ? 1024u
+                                                                                                                : 512u);
         if (bs == 1024u)
             return launch_bs<MODE, COUNT, VEC, STAGE, NODE, 1024>(T, tu, t, src, dst, sport, dport, proto, n, out,
                                                                   counters, st, hist, stage, items);
