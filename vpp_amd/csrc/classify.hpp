@@ -75,6 +75,7 @@ struct DevLoader {
     PG_HD uint32_t at_byte(uint32_t off) const {
         return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(b) + off);
     }
+    PG_HD uint32_t u16(uint32_t i) const { return reinterpret_cast<const uint16_t*>(b)[i]; }  // halfword i
     PG_HD W2 u2(uint32_t i) const {
 #if defined(__HIP_DEVICE_COMPILE__)
         const uint2 v = *reinterpret_cast<const uint2*>(b + i);
@@ -398,13 +399,9 @@ struct NodeEval {
         for (int j = 0; j < Q; j++) {
             const uint32_t tt = act[j] ? (uint32_t)t[j] : 0u;
             const W4 ti = img.u4(N.tabinfo + 4u * tt);  // {cross base, nkc | covered << 31, common row, 0}
-            const uint32_t ki = tt * N.gk + gk[j];
-            const uint32_t lk = (img.u32(N.kmap + (ki >> 1)) >> ((ki & 1u) * 16u)) & 0xFFFFu;
+            const uint32_t lk = img.u16(2u * N.kmap + (tt << N.gk_shift) + gk[j]);
             uint32_t cw = 0;
-            if (CM) {
-                const uint32_t b = tt * N.n_ipc + ca[j];
-                cw = img.u32(N.cmap + (b >> 5u)) >> (b & 31u);
-            }
+            if (CM) cw = img.u32(N.cmap + (tt << N.cmap_shift) + (ca[j] >> 5u)) >> (ca[j] & 31u);
             on[j] = act[j] && k[j] < kWalkKeyLimit && (ti.y >> 31);
             cm[j] = CM && (cw & 1u);
             pos[j] = cm[j] ? ti.z + lk : ti.x + ca[j] * (ti.y & 0xFFFFu) + lk;

@@ -49,10 +49,11 @@ struct DevTable {          // 32 B: two 16-B loads
 //                 u32[gk] (self words: A << 10 at byte A, so a finished lookup re-reads itself
 //                 and every lookup has the trie's depth) | ipinfo uint2[n_ipc] {interface,
 //                 tin | tout << 16} | tabinfo
-//                 uint4[T] {cross base, nkc | covered << 31, common row, 0} | kmap u16[T][gk]
+//                 uint4[T] {cross base, nkc | covered << 31, common row, 0} | kmap u16[T][2^gk_shift]
 //                 (local key class) | the words up to img_words_base are the base image;
 //                 then the common-row section (cmap != 0): per covered table its most
-//                 frequent cross row (u32[nkc], at tabinfo.z) and a bitmap over [T][n_ipc],
+//                 frequent cross row (u32[nkc], at tabinfo.z) and a bitmap over [T][n_ipc]
+//                 (rows of 2^cmap_shift words),
 //                 bit set = that (table, ip class) row equals the table's common row, so the
 //                 entry is read from the (LDS-staged) image instead of the cross table
 //   cross  u32[]  per covered table, [ip class][local key class] -> verdict, or kNodeList |
@@ -78,6 +79,10 @@ struct DevNode {
     uint32_t ip_depth, key_depth, ipself, kself;
     uint32_t ipinfo, tabinfo, kmap;  // word offsets in img
     uint32_t gk;           // node key classes
+    // row strides as shifts (rows padded to powers of two, so a row address is one shifted add):
+    // kmap: table t's u16 row at halfword (kmap * 2) + (t << gk_shift); common-row bitmap:
+    // table t's row of n_ipc bits at word cmap + (t << cmap_shift)
+    uint32_t gk_shift, cmap_shift;
     uint32_t n_ipc;        // node IP classes
     uint32_t n_pair;       // covered PAIR tables (0: the evaluations skip the PAIR steps)
 };

@@ -848,10 +848,12 @@ void build_common_rows(HostTableSet& h, const std::vector<uint32_t>& cov, const 
     std::vector<uint32_t>& img = h.node_img;
     DevNode& N = h.node;
     const uint32_t T = (uint32_t)h.tabs.size(), G = N.n_ipc;
-    const uint64_t bits = (uint64_t)T * G;
+    uint32_t rs = 0;  // bitmap row: G bits in 2^rs words
+    while ((32ull << rs) < G) rs++;
+    const uint64_t bits = (uint64_t)T << (rs + 5);
     if (!tu.node_common || bits > kCommonMapMaxBits) return;
     const std::vector<uint32_t>& X = h.node_cross;
-    std::vector<uint32_t> sec, map((size_t)((bits + 31) / 32), 0);
+    std::vector<uint32_t> sec, map((size_t)(bits / 32), 0);
     std::vector<uint32_t> crow(T, 0);
     for (uint32_t t : cov) {
         const uint32_t base = img[N.tabinfo + 4 * t], nk = an[t]->nkc;
@@ -872,16 +874,14 @@ void build_common_rows(HostTableSet& h, const std::vector<uint32_t>& cov, const 
         crow[t] = (uint32_t)sec.size();
         sec.insert(sec.end(), row(best), row(best) + nk);
         for (uint32_t g = 0; g < G; g++)
-            if (std::equal(row(g), row(g) + nk, row(best))) {
-                const uint64_t b = (uint64_t)t * G + g;
-                map[b >> 5] |= 1u << (b & 31u);
-            }
+            if (std::equal(row(g), row(g) + nk, row(best))) map[((size_t)t << rs) + (g >> 5)] |= 1u << (g & 31u);
     }
     while (sec.size() % 4) sec.push_back(0);
     const uint32_t s0 = (uint32_t)img.size();
     for (uint32_t t : cov) img[N.tabinfo + 4 * t + 2] = s0 + crow[t];
     img.insert(img.end(), sec.begin(), sec.end());
     N.cmap = (uint32_t)img.size();
+    N.cmap_shift = rs;
     img.insert(img.end(), map.begin(), map.end());
     while (img.size() % 4) img.push_back(0);
     N.img_words = (uint32_t)img.size();
@@ -1027,8 +1027,10 @@ bool build_node(HostTableSet& h, const std::vector<TableAnalysis*>& an, const st
     while (img.size() % 4) img.push_back(0);
     N.tabinfo = (uint32_t)img.size();
     img.resize(img.size() + 4 * (size_t)T, 0);
+    N.gk_shift = 0;
+    while ((1u << N.gk_shift) < GK) N.gk_shift++;
     N.kmap = (uint32_t)img.size();
-    img.resize(img.size() + ((size_t)T * GK + 1) / 2, 0);
+    img.resize(img.size() + (((size_t)T << N.gk_shift) + 1) / 2, 0);
     while (img.size() % 4) img.push_back(0);
     // PAIR tables: per node IP class, the table's src class | dst class << 16
     std::vector<uint32_t> pmap_off(PC);
@@ -1056,7 +1058,7 @@ bool build_node(HostTableSet& h, const std::vector<TableAnalysis*>& an, const st
         img[N.tabinfo + 4 * t] = (uint32_t)X.size();
         img[N.tabinfo + 4 * t + 1] = A.nkc | 0x80000000u;
         for (uint32_t g = 0; g < GK; g++) {
-            const uint32_t ki = t * GK + g;
+            const uint32_t ki = (t << N.gk_shift) + g;
             img[N.kmap + ki / 2] |= kc_key[g][c] << ((ki & 1u) * 16u);
         }
         if (A.pair) {  // {pair map base, nkc | covered | PAIR, verdicts base, class map | ndc << 16}
