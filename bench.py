@@ -94,12 +94,19 @@ def main():
         raise SystemExit("bench.py: --gpus %d but the launcher started %d ranks" % (a.gpus, world))
     if a.cpu_dry_run:
         return dry_run(a, rank, world)
-    if world > 1:
+    # under torchrun (the driver's N > 1 launch, or --nproc-per-node 1 to rehearse it on one
+    # GPU) the process group, barriers, max-over-ranks timing and the library's RCCL counter
+    # all-reduce all run, whatever the world size
+    launched = "WORLD_SIZE" in os.environ
+    # stdout carries the ONE JSON line: whatever native libraries print there (RCCL's version
+    # banner at communicator init) goes to stderr instead
+    sys.stdout.flush()
+    json_out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
+    torch.cuda.set_device(local)
+    if launched:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(local)
     kw = {"n_tuples": a.tuples} if a.tuples else {}
     if a.rules:
         if a.config != 2:
@@ -128,7 +135,7 @@ def main():
     # kernel duration rocprofv3 reports.
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize()
-    if world > 1:
+    if launched:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -137,7 +144,7 @@ def main():
         D.classify(e, w.mode, w.table_id, b, out, counters=cptr)
     ev1.record()
     torch.cuda.synchronize()
-    if world > 1:
+    if launched:
         dist.barrier()
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
@@ -150,7 +157,7 @@ def main():
     # statscollector path: the per-rule hit counters of one counted pass over every rank's
     # shard, summed by RCCL through the library's own communicator (pg_allreduce_counters)
     allreduce = None
-    if world > 1:
+    if launched:
         allreduce = counter_allreduce(e, w, b, out, rank, world)
 
     bpt, fields = bytes_per_tuple(w)
@@ -183,8 +190,8 @@ def main():
         line["cpu_baseline"], line["parity_sample"] = cpu_baseline(w, b, out, a.cpu_sample, a.faithful_seconds,
                                                                    a.cpu_seconds)
     if rank == 0:
-        print(json.dumps(line), flush=True)
-    if world > 1:
+        print(json.dumps(line), file=json_out, flush=True)
+    if launched:
         dist.destroy_process_group()
 
 

@@ -41,14 +41,14 @@ def allreduce_counters(counters, group=None):
     every rank because every rank compiles the same committed ACLs."""
     if counters.dtype != torch.int64:
         raise TypeError("counters must be int64 (u64 slots)")
-    if dist.is_initialized() and dist.get_world_size(group) > 1:
+    if dist.is_initialized():
         dist.all_reduce(counters, op=dist.ReduceOp.SUM, group=group)
     return counters
 
 
 def sum_over_ranks(value, device):
     """Sum of an integer over all ranks (tuples of the whole job)."""
-    if not (dist.is_initialized() and dist.get_world_size() > 1):
+    if not dist.is_initialized():
         return int(value)
     t = torch.tensor([int(value)], dtype=torch.int64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.SUM)
@@ -57,7 +57,7 @@ def sum_over_ranks(value, device):
 
 def max_over_ranks(value, device):
     """Max of a float over all ranks (the bench's wall time)."""
-    if not (dist.is_initialized() and dist.get_world_size() > 1):
+    if not dist.is_initialized():
         return value
     t = torch.tensor([value], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
