@@ -1,5 +1,6 @@
 // extern "C" boundary (include/policygpu.h). Converts the flat C structs into the host
 // model, forwards to the renderer / engine and maps failures to PG_* codes + last_error.
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -744,9 +745,10 @@ int pg_classify(pg_ctx* ctx, int mode, int table_id, const pg_tuple_soa* t, uint
     if (!t->src_ip || !t->dst_ip || !t->dst_port || !t->proto || (mode == PG_MODE_CONN && !t->src_port))
         return fail(ctx, PG_EINVAL, "missing tuple field");
     std::string err;
+    static const bool skip_mark = std::getenv("PG_PROBE_SKIP_MARK") != nullptr;  // measurement aid only
     if (dev_classify(T, ctx->eng.tune, mode, table_id, t->src_ip, t->dst_ip, t->src_port, t->dst_port, t->proto, n,
                      out, (unsigned long long*)counters, stream, &err) != 0 ||
-        dev_mark_use(ctx->eng.cur, stream, &err) != 0)
+        (!skip_mark && dev_mark_use(ctx->eng.cur, stream, counters != nullptr, &err) != 0))
         return fail(ctx, PG_EIO, err);
     return PG_OK;
     GUARD_END(ctx)
@@ -762,7 +764,7 @@ int pg_classify_linear(pg_ctx* ctx, int table_id, const pg_tuple_soa* t, uint64_
     if (table_id < 0 || (uint32_t)table_id >= T.n_tables) return fail(ctx, PG_EINVAL, "table id out of range");
     std::string err;
     if (dev_classify_linear(T, table_id, t->src_ip, t->dst_ip, t->dst_port, t->proto, n, out, stream, &err) != 0 ||
-        dev_mark_use(ctx->eng.cur, stream, &err) != 0)
+        dev_mark_use(ctx->eng.cur, stream, false, &err) != 0)
         return fail(ctx, PG_EIO, err);
     return PG_OK;
     GUARD_END(ctx)

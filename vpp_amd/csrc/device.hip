@@ -45,10 +45,15 @@ struct DeviceBuffers {
     DevTableSet view{};
     std::vector<DevTable> host_tabs;
     std::vector<uint32_t> host_blob_words, host_blob_prefix;
-    // streams that launched kernels reading this set, with an event recorded after the last
+    // streams that launched kernels reading this set, with events recorded after the last
     // launch on each: the set is freed (and counters read) once those have completed, without
-    // a device-wide synchronisation
-    std::vector<std::pair<hipStream_t, hipEvent_t>> uses;
+    // a device-wide synchronisation (dev_mark_use)
+    struct Use {
+        hipStream_t s;
+        hipEvent_t plain, fenced;
+        bool plain_rec, fenced_rec;
+    };
+    std::vector<Use> uses;
 };
 
 const DevTableSet& dev_view(const DeviceBuffers* b) { return b->view; }
@@ -91,22 +96,33 @@ int dev_stream_sync(void* stream, std::string* err) {
     return 0;
 }
 
-int dev_mark_use(DeviceBuffers* b, void* stream, std::string* err) {
+// Completion events per stream: `fenced` after launches that wrote hit counters (the
+// system-scope release makes them visible to the counter read-back), a fence-free one after the
+// others -- freeing a set needs only that its readers have finished, and a system-scope fence
+// per record cost ~3 us per back-to-back launch on MI355X (tools/gap_probe.py: 130.2 -> 127.1 us
+// per config-2 launch without it)
+int dev_mark_use(DeviceBuffers* b, void* stream, bool fenced, std::string* err) {
     const hipStream_t s = (hipStream_t)stream;
     for (auto& u : b->uses)
-        if (u.first == s) {
-            HIPCHK(hipEventRecord(u.second, s));
+        if (u.s == s) {
+            HIPCHK(hipEventRecord(fenced ? u.fenced : u.plain, s));
+            (fenced ? u.fenced_rec : u.plain_rec) = true;
             return 0;
         }
-    hipEvent_t e;
-    HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    b->uses.push_back({s, e});
-    HIPCHK(hipEventRecord(e, s));
+    DeviceBuffers::Use u{s, nullptr, nullptr, false, false};
+    HIPCHK(hipEventCreateWithFlags(&u.plain, hipEventDisableTiming | hipEventDisableSystemFence));
+    HIPCHK(hipEventCreateWithFlags(&u.fenced, hipEventDisableTiming));
+    b->uses.push_back(u);
+    HIPCHK(hipEventRecord(fenced ? u.fenced : u.plain, s));
+    (fenced ? b->uses.back().fenced_rec : b->uses.back().plain_rec) = true;
     return 0;
 }
 
 int dev_wait_uses(DeviceBuffers* b, std::string* err) {
-    for (auto& u : b->uses) HIPCHK(hipEventSynchronize(u.second));
+    for (auto& u : b->uses) {
+        if (u.plain_rec) HIPCHK(hipEventSynchronize(u.plain));
+        if (u.fenced_rec) HIPCHK(hipEventSynchronize(u.fenced));
+    }
     return 0;
 }
 
@@ -180,8 +196,10 @@ DeviceBuffers* dev_upload(const HostTableSet& h, std::string* err) {
 void dev_free(DeviceBuffers* b) {
     if (!b) return;
     for (auto& u : b->uses) {  // launches that read the set have completed
-        (void)hipEventSynchronize(u.second);
-        (void)hipEventDestroy(u.second);
+        if (u.plain_rec) (void)hipEventSynchronize(u.plain);
+        if (u.fenced_rec) (void)hipEventSynchronize(u.fenced);
+        (void)hipEventDestroy(u.plain);
+        (void)hipEventDestroy(u.fenced);
     }
     dev_release(b->blob);
     delete b;

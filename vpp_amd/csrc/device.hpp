@@ -231,7 +231,7 @@ int dev_copy_h2d(void* dst, const void* src, size_t bytes, std::string* err);
 int dev_sync(std::string* err);
 int dev_stream_sync(void* stream, std::string* err);
 // record that `stream` launched kernels reading table set b (dev_free / dev_wait_uses wait for them)
-int dev_mark_use(DeviceBuffers* b, void* stream, std::string* err);
+int dev_mark_use(DeviceBuffers* b, void* stream, bool fenced, std::string* err);
 int dev_wait_uses(DeviceBuffers* b, std::string* err);
 // RCCL communicators (opaque ncclComm_t), librccl opened on first use
 int dev_comm_unique_id(uint8_t* id /* 128 B */, std::string* err);
