@@ -1,0 +1,11 @@
+# windowed hit-counter histogram vs round-2 HEAD: configs 5 / 2 / 3-with-counters unchanged?
+set -o pipefail
+O=gpurun_out/abhist2; mkdir -p $O
+timeout -k 10 500 python -u -m pytest tests/test_gpu_configs.py -m gpu -x -q --timeout 300 --timeout-method thread -k "counters" > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 1; }
+tail -1 $O/tests.log
+run() { VPP_AMD_LIB=$PWD/vpp_amd/$1 timeout -k 10 250 python tools/sweep.py --rounds 2 --reps 8 "${@:2}" | sed "s/^/$1 /" | tee -a $O/sweep.log; }
+for r in 1 2; do for lib in libpolicygpu_base.so libpolicygpu.so; do
+  run $lib --config 5 --counters || exit 1
+  run $lib --config 2 --counters || exit 1
+done; done
+run libpolicygpu.so --config 4 --counters || exit 1

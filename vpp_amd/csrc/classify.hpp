@@ -210,6 +210,10 @@ PG_HD void probe_q(const DevTableSet& T, const uint32_t (&ip)[Q], End (&e)[Q]) {
 struct Hist {
     uint32_t* lds;
     unsigned long long* glob;
+    // device, lds set: cells [0, wn) count slots [wbase, wbase + wn), cell wn counts slot xslot,
+    // other slots go to glob (device.hip k_classify)
+    uint32_t wbase = 0, wn = 0xFFFFFFFFu, xslot = 0xFFFFFFFFu;
+    bool full = true;  // the window holds every slot (wave-uniform: the common case costs no test)
     PG_HD void inc(uint32_t slot) const {
 #if defined(__HIP_DEVICE_COMPILE__) && defined(PG_PROBE_NOINC)  // measurement build only
         if (slot == 0xFFFFFFFFu) lds[0] = 0;
@@ -226,7 +230,9 @@ struct Hist {
                 const unsigned long long m = __ballot(slot == lead);
                 if (slot == lead) {
                     if (__lane_id() == (unsigned)(__ffsll((long long)m) - 1)) {
-                        if (lds) atomicAdd(&lds[lead], (uint32_t)__popcll(m));
+                        const uint32_t c = lead - wbase;
+                        if (lds && c < wn) atomicAdd(&lds[c], (uint32_t)__popcll(m));
+                        else if (lds && lead == xslot) atomicAdd(&lds[wn], (uint32_t)__popcll(m));
                         else if (glob) atomicAdd(&glob[lead], (unsigned long long)__popcll(m));
                     }
                     done = true;
@@ -234,7 +240,10 @@ struct Hist {
             }
         }
         if (!done) {
-            if (lds) atomicAdd(&lds[slot], 1u);
+            const uint32_t c = slot - wbase;
+            if (lds && full) atomicAdd(&lds[slot], 1u);
+            else if (lds && c < wn) atomicAdd(&lds[c], 1u);
+            else if (lds && slot == xslot) atomicAdd(&lds[wn], 1u);
             else if (glob) atomicAdd(&glob[slot], 1ull);
         }
 #else

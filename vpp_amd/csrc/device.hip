@@ -319,7 +319,7 @@ int dev_comm_allreduce_u64(void* const* comms, unsigned long long* const* bufs, 
 }
 
 constexpr int kBlock = 256;
-constexpr uint32_t kLdsHistMax = 16384;  // slots kept in LDS (64 KiB)
+constexpr uint32_t kLdsHistMax = 16384;  // hit-counter cells kept in LDS (64 KiB): a window + 1
 
 // Tuple streams are read once and verdicts written once: issued with the non-temporal
 // policy (A/B in one process with tools/sweep.py: +3-4 % on config 2; PG_NT_STREAM=0 builds
@@ -435,27 +435,32 @@ __device__ __forceinline__ void st_words(const Words<NW>& v, uint32_t* p) {
 #ifndef PG_CONN_COUNT_WPE
 #define PG_CONN_COUNT_WPE 8
 #endif
-template <int MODE, bool COUNT, bool NODE>
+// SINGLE over a blob in HBM (STAGE 0 / 2, the dst-free variants included): 66 registers at four
+// tuples per chunk hold it to three 512-thread workgroups per CU; a 64-register cap spills
+#ifndef PG_SINGLE_HBM_WPE  // (A/B on MI355X, config 4: 8 = 164.6 Gpps with 2 spills, 1 = 175.7)
+#define PG_SINGLE_HBM_WPE 1
+#endif
+template <int MODE, bool COUNT, bool NODE, int STAGE = 1>
 constexpr int kernel_wpe() {
-    return !NODE ? 1 : (MODE == 2 && COUNT ? PG_CONN_COUNT_WPE : PG_NODE_WPE);
+    return !NODE ? (MODE == 0 && ((STAGE & 7) == 0 || (STAGE & 7) == 2) ? PG_SINGLE_HBM_WPE : 1)
+                 : (MODE == 2 && COUNT ? PG_CONN_COUNT_WPE : PG_NODE_WPE);
 }
 // STAGE_ + 8 (SINGLE, STAGE 0-2): the table is dst-free (kFlagDstFree: no rule tests dst), so
 // the dst stream is not read
 template <int MODE, bool COUNT, bool VEC, int STAGE_, bool NODE, int BS>
-__global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(kernel_wpe<MODE, COUNT, NODE>())))
+__global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(kernel_wpe<MODE, COUNT, NODE, STAGE_>())))
 void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
                                                      const uint32_t* __restrict__ dst,
                                                      const uint16_t* __restrict__ sport,
                                                      const uint16_t* __restrict__ dport,
                                                      const uint8_t* __restrict__ proto, uint64_t n,
                                                      uint32_t* __restrict__ out, unsigned long long* counters,
-                                                     uint32_t stage_words) {
+                                                     uint32_t stage_words, uint32_t hist_cells) {
     constexpr int STAGE = STAGE_ & 7;
     constexpr bool NODST = MODE == 0 && STAGE_ >= 8;
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     uint32_t* hist = smem + (STAGE ? stage_words : 0u);
     Hist h{nullptr, counters};
-    const bool use_lds = COUNT && T.n_slots <= kLdsHistMax;
     DevTable tab0{};
     const uint32_t* blobs = T.blobs;
     DevLoader img{T.node.img};
@@ -477,11 +482,23 @@ void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
     }
     // STAGE 2: only the header and src-trie root of a large blob are in LDS
     const uint32_t* rootb = (MODE == 0 && STAGE == 2) ? smem : nullptr;
-    if (COUNT && use_lds) {
-        for (uint32_t i = threadIdx.x; i < T.n_slots; i += BS) hist[i] = 0;
+    // hit counters: an LDS histogram of the window [wbase, wbase + wn) of slots plus one cell for
+    // slot xslot, flushed with one u64 atomic per non-zero cell; slots outside go to global
+    // atomics. Every slot fits the window unless the table set has more than kLdsHistMax - 1;
+    // then the window is a SINGLE table's first rules (first-match traffic favours them:
+    // config 4's Zipf depth) and the extra cell its default-deny slot (node modes: "no ACL")
+    const uint32_t wn = COUNT ? hist_cells : 0u;
+    const uint32_t wbase = (MODE == 0 && wn < T.n_slots) ? min(tab0.rule_base, T.n_slots - wn) : 0u;
+    const uint32_t xslot = MODE == 0 ? (tab0.dflt & kSlotMask) : T.slot_noacl;
+    if (COUNT) {
+        for (uint32_t i = threadIdx.x; i <= wn; i += BS) hist[i] = 0;
         h.lds = hist;
+        h.wbase = wbase;
+        h.wn = wn;
+        h.xslot = xslot;
+        h.full = wn >= T.n_slots;
     }
-    if (STAGE || (COUNT && use_lds)) __syncthreads();
+    if (STAGE || COUNT) __syncthreads();
     const uint64_t stride = (uint64_t)gridDim.x * BS;
     const uint64_t first = (uint64_t)blockIdx.x * BS + threadIdx.x;
     // full groups of P tuples per lane (P = PG_TPL): SoA fields read with 16/8/4-byte loads per
@@ -585,12 +602,12 @@ void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
         else classify_q<MODE, COUNT, 1, STAGE == 1 && PG_PRED>(T, blobs, tab0, s1, d1, sp1, dp1, pr1, h, o, rootb);
         out[i] = o[0];
     }
-    if (COUNT && use_lds) {
+    if (COUNT) {
         __syncthreads();
-        for (uint32_t i = threadIdx.x; i < T.n_slots; i += BS) {
+        for (uint32_t i = threadIdx.x; i <= wn; i += BS) {
             const uint32_t v = hist[i];
 #if !defined(PG_PROBE_NOFLUSH)  // measurement build only: the histogram is not flushed
-            if (v) atomicAdd(&counters[i], (unsigned long long)v);
+            if (v) atomicAdd(&counters[i < wn ? wbase + i : xslot], (unsigned long long)v);
 #endif
         }
     }
@@ -802,8 +819,9 @@ static void launch_bs(const DevTableSet& T, const Tuning& tu, int t, const uint3
                       unsigned long long* counters, hipStream_t st, size_t hist, uint32_t stage, uint64_t items) {
     auto k = k_classify<MODE, COUNT, VEC, STAGE, NODE, BS>;
     const size_t lds = hist + (size_t)stage * 4;
+    const uint32_t cells = hist ? (uint32_t)(hist / 4 - 1) : 0u;  // window cells (+ the extra one)
     hipLaunchKernelGGL(k, dim3(grid_resident(k, BS, lds, items, tu.blocks_per_cu)), dim3(BS), lds, st, T, t, src, dst, sport, dport,
-                       proto, n, out, counters, stage);
+                       proto, n, out, counters, stage, cells);
 }
 
 // Workgroup size: a staged image is shared by the workgroup, so larger workgroups hold more
@@ -853,7 +871,10 @@ template <int MODE, bool COUNT, bool VEC>
 static void launch_classify(const DevTableSet& T, const Tuning& tu, int t, const uint32_t* src, const uint32_t* dst,
                             const uint16_t* sport, const uint16_t* dport, const uint8_t* proto, uint64_t n,
                             uint32_t* out, unsigned long long* counters, hipStream_t st) {
-    const size_t hist = (COUNT && T.n_slots <= kLdsHistMax) ? T.n_slots * 4 : 0;
+    // hit-counter LDS histogram: every slot + 1 cell, or (more slots than fit) a window of
+    // hist_window cells + 1 (k_classify)
+    const uint32_t cells = T.n_slots <= kLdsHistMax - 1u ? T.n_slots : std::min(tu.hist_window, kLdsHistMax - 1u);
+    const size_t hist = COUNT ? ((size_t)cells + 1u) * 4 : 0;
     const uint64_t items = VEC ? (n + PG_TPL - 1) / PG_TPL : n;
     if constexpr (MODE == 0) {
         const DevTable& hd = T.host_tabs[t];

@@ -136,7 +136,7 @@ struct Tuning {
     uint32_t lc_lds = 4096;        // LC rebuild of LDS-sized blobs of at least this many words (0 = off)
     uint32_t lc_dense12 = 16;      // boundaries in a child's span that earn it a 12-bit stride
     uint32_t lc_max_stride = 16;   // widest level-compressed stride (12, 16, 18)
-    uint32_t lc_root_bits = 12;    // src-trie root stride cap of HBM-resident (level-compressed) blobs
+    uint32_t lc_root_bits = 13;    // src-trie root stride cap of HBM-resident (level-compressed) blobs
     uint32_t pair = 1;             // PAIR for tables CROSS cannot take (0 = CAND, 2 = wherever it fits)
     uint32_t node_build = 1;       // build the node classifier (PERPOD / CONN)
     uint32_t node_root_bits = 12;  // its IPv4 / key trie root stride cap (4..16)
@@ -153,6 +153,7 @@ struct Tuning {
     uint32_t node_path = 1;        // PERPOD / CONN through the node classifier when built
     uint32_t node_common_lds_max = 80u << 10;    // LDS bytes up to which the common-row section is staged
     uint32_t block_stage = 0;      // workgroup size of LDS-staged launches (0 = per mode)
+    uint32_t hist_window = 4096;   // LDS hit-counter cells when the slots exceed the LDS histogram
 };
 // key -> field; 0 ok, -1 unknown key or value out of range. *compiler: the key changes how
 // tables are compiled (the context recompiles on its next use).
