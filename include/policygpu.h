@@ -149,9 +149,9 @@ int pg_ctx_device(const pg_ctx* ctx);
  * "node_stage_max_words" (largest node image staged in LDS, default 16384),
  * "node_common_lds_max" (LDS bytes up to which the node image's common-row section is staged,
  * default 80 KiB), "block_stage" (workgroup size of LDS-staged classify launches: 256, 512 or
- * 1024; default 0 = per mode), "hist_window" (hit counters of a table set with more than 16383
- * slots: LDS cells kept for the classified table's first rules, the rest counted with global
- * atomics; default 4096);
+ * 1024; default 0 = per mode), "hist_window" (hit counters of a table set with more than 16382
+ * slots: LDS cells kept for the classified table's first rules -- its default-deny slot and last
+ * rule always get one -- the rest counted with global atomics; default 4096);
  * table compiler (the context recompiles and re-uploads on its next use; hit counters restart)
  * -- "root_bits_max" (cap of the src/key trie root stride, 4..16, default 16), "node_build"
  * (1/0: build the node classifier for PERPOD / CONN, default 1), "node_root_bits" (its IPv4 /

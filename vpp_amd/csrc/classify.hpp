@@ -210,9 +210,9 @@ PG_HD void probe_q(const DevTableSet& T, const uint32_t (&ip)[Q], End (&e)[Q]) {
 struct Hist {
     uint32_t* lds;
     unsigned long long* glob;
-    // device, lds set: cells [0, wn) count slots [wbase, wbase + wn), cell wn counts slot xslot,
-    // other slots go to glob (device.hip k_classify)
-    uint32_t wbase = 0, wn = 0xFFFFFFFFu, xslot = 0xFFFFFFFFu;
+    // device, lds set: cells [0, wn) count slots [wbase, wbase + wn), cells wn and wn + 1 count
+    // slots xslot and xslot1, other slots go to glob (device.hip k_classify)
+    uint32_t wbase = 0, wn = 0xFFFFFFFFu, xslot = 0xFFFFFFFFu, xslot1 = 0xFFFFFFFFu;
     bool full = true;  // the window holds every slot (wave-uniform: the common case costs no test)
     PG_HD void inc(uint32_t slot) const {
 #if defined(__HIP_DEVICE_COMPILE__) && defined(PG_PROBE_NOINC)  // measurement build only
@@ -233,6 +233,7 @@ struct Hist {
                         const uint32_t c = lead - wbase;
                         if (lds && c < wn) atomicAdd(&lds[c], (uint32_t)__popcll(m));
                         else if (lds && lead == xslot) atomicAdd(&lds[wn], (uint32_t)__popcll(m));
+                        else if (lds && lead == xslot1) atomicAdd(&lds[wn + 1], (uint32_t)__popcll(m));
                         else if (glob) atomicAdd(&glob[lead], (unsigned long long)__popcll(m));
                     }
                     done = true;
@@ -244,6 +245,7 @@ struct Hist {
             if (lds && full) atomicAdd(&lds[slot], 1u);
             else if (lds && c < wn) atomicAdd(&lds[c], 1u);
             else if (lds && slot == xslot) atomicAdd(&lds[wn], 1u);
+            else if (lds && slot == xslot1) atomicAdd(&lds[wn + 1], 1u);
             else if (glob) atomicAdd(&glob[slot], 1ull);
         }
 #else

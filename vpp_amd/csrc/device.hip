@@ -482,20 +482,24 @@ void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
     }
     // STAGE 2: only the header and src-trie root of a large blob are in LDS
     const uint32_t* rootb = (MODE == 0 && STAGE == 2) ? smem : nullptr;
-    // hit counters: an LDS histogram of the window [wbase, wbase + wn) of slots plus one cell for
-    // slot xslot, flushed with one u64 atomic per non-zero cell; slots outside go to global
-    // atomics. Every slot fits the window unless the table set has more than kLdsHistMax - 1;
-    // then the window is a SINGLE table's first rules (first-match traffic favours them:
-    // config 4's Zipf depth) and the extra cell its default-deny slot (node modes: "no ACL")
+    // hit counters: an LDS histogram of the window [wbase, wbase + wn) of slots plus cells for
+    // slots xslot and xslot1, flushed with one u64 atomic per non-zero cell; slots outside go to
+    // global atomics. Every slot fits the window unless the table set has more than
+    // kLdsHistMax - 2; then the window is a SINGLE table's first rules (first-match traffic
+    // favours them: config 4's Zipf depth) and the extra cells its default-deny slot and its
+    // last rule (a deny-the-rest / allow-all catch-all takes every unmatched packet: a single
+    // global address would serialise them); node modes: "no ACL", "unresolved"
     const uint32_t wn = COUNT ? hist_cells : 0u;
     const uint32_t wbase = (MODE == 0 && wn < T.n_slots) ? min(tab0.rule_base, T.n_slots - wn) : 0u;
     const uint32_t xslot = MODE == 0 ? (tab0.dflt & kSlotMask) : T.slot_noacl;
+    const uint32_t xslot1 = MODE == 0 ? (tab0.n_rules ? tab0.rule_base + tab0.n_rules - 1u : xslot) : T.slot_unresolved;
     if (COUNT) {
-        for (uint32_t i = threadIdx.x; i <= wn; i += BS) hist[i] = 0;
+        for (uint32_t i = threadIdx.x; i <= wn + 1u; i += BS) hist[i] = 0;
         h.lds = hist;
         h.wbase = wbase;
         h.wn = wn;
         h.xslot = xslot;
+        h.xslot1 = xslot1;
         h.full = wn >= T.n_slots;
     }
     if (STAGE || COUNT) __syncthreads();
@@ -604,10 +608,10 @@ void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
     }
     if (COUNT) {
         __syncthreads();
-        for (uint32_t i = threadIdx.x; i <= wn; i += BS) {
+        for (uint32_t i = threadIdx.x; i <= wn + 1u; i += BS) {
             const uint32_t v = hist[i];
 #if !defined(PG_PROBE_NOFLUSH)  // measurement build only: the histogram is not flushed
-            if (v) atomicAdd(&counters[i < wn ? wbase + i : xslot], (unsigned long long)v);
+            if (v) atomicAdd(&counters[i < wn ? wbase + i : (i == wn ? xslot : xslot1)], (unsigned long long)v);
 #endif
         }
     }
@@ -819,7 +823,7 @@ static void launch_bs(const DevTableSet& T, const Tuning& tu, int t, const uint3
                       unsigned long long* counters, hipStream_t st, size_t hist, uint32_t stage, uint64_t items) {
     auto k = k_classify<MODE, COUNT, VEC, STAGE, NODE, BS>;
     const size_t lds = hist + (size_t)stage * 4;
-    const uint32_t cells = hist ? (uint32_t)(hist / 4 - 1) : 0u;  // window cells (+ the extra one)
+    const uint32_t cells = hist ? (uint32_t)(hist / 4 - 2) : 0u;  // window cells (+ the two extra ones)
     hipLaunchKernelGGL(k, dim3(grid_resident(k, BS, lds, items, tu.blocks_per_cu)), dim3(BS), lds, st, T, t, src, dst, sport, dport,
                        proto, n, out, counters, stage, cells);
 }
@@ -873,8 +877,8 @@ static void launch_classify(const DevTableSet& T, const Tuning& tu, int t, const
                             uint32_t* out, unsigned long long* counters, hipStream_t st) {
     // hit-counter LDS histogram: every slot + 1 cell, or (more slots than fit) a window of
     // hist_window cells + 1 (k_classify)
-    const uint32_t cells = T.n_slots <= kLdsHistMax - 1u ? T.n_slots : std::min(tu.hist_window, kLdsHistMax - 1u);
-    const size_t hist = COUNT ? ((size_t)cells + 1u) * 4 : 0;
+    const uint32_t cells = T.n_slots <= kLdsHistMax - 2u ? T.n_slots : std::min(tu.hist_window, kLdsHistMax - 2u);
+    const size_t hist = COUNT ? ((size_t)cells + 2u) * 4 : 0;
     const uint64_t items = VEC ? (n + PG_TPL - 1) / PG_TPL : n;
     if constexpr (MODE == 0) {
         const DevTable& hd = T.host_tabs[t];

@@ -45,7 +45,7 @@ const Knob kKnobs[] = {
     {"node_path", &Tuning::node_path, 0, 1, false},
     {"node_common_lds_max", &Tuning::node_common_lds_max, 0, 160 << 10, false},
     {"block_stage", &Tuning::block_stage, 0, 1024, false},
-    {"hist_window", &Tuning::hist_window, 1, 16383, false},
+    {"hist_window", &Tuning::hist_window, 1, 16382, false},
 };
 bool Knob::allowed(int v) const {
     if (field == &Tuning::lc_max_stride) return v == 12 || v == 16 || v == 18;
