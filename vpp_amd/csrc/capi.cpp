@@ -478,7 +478,7 @@ int pg_debug_walk_blob(pg_ctx* ctx, const char* acl_name, const uint32_t* src, c
             const uint32_t s1[1] = {src[i]}, dp1[1] = {dst_port[i]}, pr1[1] = {proto[i]};
             uint32_t w1[1];
             const uint32_t* b = E.host.blobs.data() + hd.blob_off;
-            classify_fd_q<false, 1>(T, b, b, hd, s1, dp1, pr1, Hist{nullptr, nullptr}, w1);
+            classify_fd_q<false, 1>(T, DevLoader{b}, DevLoader{b}, hd, s1, dp1, pr1, Hist{nullptr, nullptr}, w1);
             out[i] = w1[0];
         }
         return PG_OK;

@@ -94,6 +94,35 @@ struct DevLoader {
     }
 };
 
+// Loads from the kernel's LDS image, which starts at LDS address 0 (k_classify's dynamic shared
+// memory; the kernel declares no static LDS): addresses are the offsets themselves, so a trie
+// step is a shift and a shifted add, not also an add of the (link-time zero) base.
+struct LdsLoader {
+#if defined(__HIP_DEVICE_COMPILE__)
+    template <class T>
+    static __device__ __forceinline__ T at(uint32_t byte) {
+        return *reinterpret_cast<const __attribute__((address_space(3))) T*>((uintptr_t)byte);
+    }
+    PG_HD uint32_t u32(uint32_t i) const { return at<uint32_t>(i * 4u); }
+    PG_HD uint32_t at_byte(uint32_t off) const { return at<uint32_t>(off); }
+    PG_HD uint32_t u16(uint32_t i) const { return at<uint16_t>(i * 2u); }
+    PG_HD W2 u2(uint32_t i) const {
+        const uint2 v = at<uint2>(i * 4u);
+        return W2{v.x, v.y};
+    }
+    PG_HD W4 u4(uint32_t i) const {
+        const uint4 v = at<uint4>(i * 4u);
+        return W4{v.x, v.y, v.z, v.w};
+    }
+#else  // host builds never instantiate it (kernels only)
+    uint32_t u32(uint32_t) const { return 0; }
+    uint32_t at_byte(uint32_t) const { return 0; }
+    uint32_t u16(uint32_t) const { return 0; }
+    W2 u2(uint32_t) const { return W2{0, 0}; }
+    W4 u4(uint32_t) const { return W4{0, 0, 0, 0}; }
+#endif
+};
+
 PG_HD DevTable load_tab(const DevTable* tabs, int32_t t) {
     const DevLoader l{reinterpret_cast<const uint32_t*>(tabs + t)};
     const W4 a = l.u4(0), c = l.u4(4);
@@ -258,15 +287,15 @@ struct Hist {
 // lockstep; ANY-protocol packets take the linear scan. prefix: the blob's prefix (its LDS copy
 // in the kernels), blob: the whole blob (the same LDS copy when it is staged whole, else HBM).
 // The dst address is not an input: no rule of an FD table tests it (engine.cpp compile).
-template <bool COUNT, int Q>
-PG_HD void classify_fd_q(const DevTableSet& T, const uint32_t* prefix, const uint32_t* blob, const DevTable& tab0,
+template <bool COUNT, int Q, class LP, class LB>
+PG_HD void classify_fd_q(const DevTableSet& T, const LP& prefix, const LB& blob, const DevTable& tab0,
                          const uint32_t (&s)[Q], const uint32_t (&dp)[Q], const uint32_t (&pr)[Q], const Hist& h,
                          uint32_t (&out)[Q]) {
     uint32_t key[Q];
     bool any = false;
     PG_UNROLL
     for (int j = 0; j < Q; j++) key[j] = pkt_key(pr[j], dp[j]), any |= key[j] >= kWalkKeyLimit;
-    fd_walk(DevLoader{prefix}, DevLoader{blob}, tab0.fsk, tab0.kroot, tab0.xoff, tab0.nkc, s, key, out);
+    fd_walk(prefix, blob, tab0.fsk, tab0.kroot, tab0.xoff, tab0.nkc, s, key, out);
     if (any) {
         PG_UNROLL
         for (int j = 0; j < Q; j++)  // no rule of an FD table tests dst (engine.cpp): any dst will do

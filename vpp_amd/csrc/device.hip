@@ -22,6 +22,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <type_traits>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -463,11 +464,13 @@ void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
     Hist h{nullptr, counters};
     DevTable tab0{};
     const uint32_t* blobs = T.blobs;
-    DevLoader img{T.node.img};
+    // the node image: its LDS copy (at LDS address 0: LdsLoader) when staged, else global memory
+    using ImgLoader = std::conditional_t<NODE && STAGE != 0, LdsLoader, DevLoader>;
+    ImgLoader img{};
+    if constexpr (NODE && STAGE == 0) img = DevLoader{T.node.img};
     if (NODE && STAGE) {
         const uint4* g = reinterpret_cast<const uint4*>(T.node.img);
         for (uint32_t i = threadIdx.x; i < stage_words / 4u; i += BS) reinterpret_cast<uint4*>(smem)[i] = g[i];
-        img.b = smem;
     }
     if (MODE == 0) {
         tab0 = load_tab(T.tabs, t);
@@ -576,7 +579,8 @@ void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
             for (int j = 0; j < QC; j++)
                 cs[j] = sv[c + j], cd[j] = dv[c + j], csp[j] = spv[c + j], cdp[j] = dpv[c + j], cpr[j] = prv[c + j];
             if constexpr (FD) {
-                classify_fd_q<COUNT, QC>(T, smem, fd_blob, tab0, cs, cdp, cpr, h, co);
+                if constexpr (STAGE == 4) classify_fd_q<COUNT, QC>(T, LdsLoader{}, LdsLoader{}, tab0, cs, cdp, cpr, h, co);
+                else classify_fd_q<COUNT, QC>(T, LdsLoader{}, DevLoader{fd_blob}, tab0, cs, cdp, cpr, h, co);
             } else if constexpr (NODE) {
                 if (c == 0)
                     classify_node_q<MODE, COUNT, QC, STAGE && PG_PRED, STAGE == 3>(T, T.node, img, cs, cd, csp, cdp, cpr, h, co, hook);
@@ -601,7 +605,8 @@ void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
         const uint32_t s1[1] = {src[i]}, d1[1] = {NEED_DST ? dst[i] : 0u},
                        sp1[1] = {MODE == 2 ? (uint32_t)sport[i] : 0u}, dp1[1] = {dport[i]}, pr1[1] = {proto[i]};
         uint32_t o[1];
-        if constexpr (FD) classify_fd_q<COUNT, 1>(T, smem, fd_blob, tab0, s1, dp1, pr1, h, o);
+        if constexpr (FD && STAGE == 4) classify_fd_q<COUNT, 1>(T, LdsLoader{}, LdsLoader{}, tab0, s1, dp1, pr1, h, o);
+        else if constexpr (FD) classify_fd_q<COUNT, 1>(T, LdsLoader{}, DevLoader{fd_blob}, tab0, s1, dp1, pr1, h, o);
         else if constexpr (NODE) classify_node_q<MODE, COUNT, 1, STAGE && PG_PRED, STAGE == 3>(T, T.node, img, s1, d1, sp1, dp1, pr1, h, o);
         else classify_q<MODE, COUNT, 1, STAGE == 1 && PG_PRED>(T, blobs, tab0, s1, d1, sp1, dp1, pr1, h, o, rootb);
         out[i] = o[0];
