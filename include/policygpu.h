@@ -163,8 +163,7 @@ int pg_ctx_device(const pg_ctx* ctx);
  * stride cap of blobs read from HBM, whose root alone a launch stages in LDS: 4..14, default
  * 12), "candi" (1/0: candidates inline in the 8-B trie entries of HBM-resident candidate tables
  * no live rule of which tests dst, default 1), "fd" (1/0: fixed-depth form of dst-independent
- * cross-product tables, default 1), "lc_node" (1/0:
- * level-compressed node tries, default 0), "node_common" (1/0: common-row section of node
+ * cross-product tables, default 1), "node_common" (1/0: common-row section of node
  * images, default 1), "pair" (1/0: the PAIR structure -- src x dst classes, then x key classes
  * -- for tables the cross product cannot take, default 1; 0 = candidate lists; 2 = wherever it
  * fits, for tests).

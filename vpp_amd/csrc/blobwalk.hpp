@@ -43,23 +43,27 @@ constexpr uint32_t kLeaf = 0x80000000u;
 constexpr uint32_t kTrieStrideShift = 26u, kTrieChildMask = (1u << kTrieStrideShift) - 1u;
 PG_HD uint32_t trie_child(uint32_t e) { return e & kTrieChildMask; }
 PG_HD uint32_t trie_stride(uint32_t e) { return (e >> kTrieStrideShift) & 31u; }
-// Node-image tries (LDS-staged): non-leaf entry = child byte offset << 10 | stride << 5 | shift
-// of the child level. The child entry of address a is at byte
-//   (e >> 10) + 4 * ((a >> (e & 31)) & ((1 << ((e >> 5) & 31)) - 1))
-// -- on the device one v_bfe_u32 (it reads only the low 5 bits of its offset and width
-// operands) and one v_lshl_add_u32.
-constexpr uint32_t kNodeChildMaxWords = 1u << 19;  // 2 MiB of image
-PG_HD constexpr uint32_t node_entry(uint32_t child_words, uint32_t stride, uint32_t shift) {
-    return (child_words * 4u) << 10 | stride << 5 | shift;
-}
-PG_HD uint32_t node_child_byte(uint32_t e, uint32_t a) {
+// Node-image tries (LDS-staged): non-leaf entry = child byte offset << 5 | stride of the child
+// level. The node tries take uniform strides below the root (min(8, bits left), fastpath.cpp
+// build_node), so the bit offset of a level's index is the same for every entry -- a per-level
+// constant the walk keeps in a scalar register (node_next_shift). The child entry of address a
+// is at byte
+//   (e >> 5) + 4 * ((a >> shift) & ((1 << (e & 31)) - 1))
+// -- on the device one v_bfe_u32 (its width operand is e itself: the hardware reads only the
+// low 5 bits), one v_lshl_add_u32 and, off the dependency chain, one shift of e.
+constexpr uint32_t kNodeChildMaxWords = 1u << 25;  // 128 MiB of image
+constexpr uint32_t kNodeStride = 8;  // stride of the levels below the root
+PG_HD constexpr uint32_t node_entry(uint32_t child_words, uint32_t stride) { return (child_words * 4u) << 5 | stride; }
+// bits below the next level, given the bits below the current one (uniform per level)
+PG_HD uint32_t node_next_shift(uint32_t rem) { return rem - (rem < kNodeStride ? rem : kNodeStride); }
+PG_HD uint32_t node_child_byte(uint32_t e, uint32_t a, uint32_t shift) {
 #if defined(__HIP_DEVICE_COMPILE__)
-    const uint32_t idx = __builtin_amdgcn_ubfe(a, e, e >> 5);
+    const uint32_t idx = __builtin_amdgcn_ubfe(a, shift, e);
 #else
-    const uint32_t w = (e >> 5) & 31u;
-    const uint32_t idx = (a >> (e & 31u)) & ((1u << w) - 1u);
+    const uint32_t w = e & 31u;
+    const uint32_t idx = shift >= 32u ? 0u : (a >> shift) & (w >= 32u ? 0xFFFFFFFFu : ((1u << w) - 1u));
 #endif
-    return (e >> 10) + (idx << 2);
+    return (e >> 5) + (idx << 2);
 }
 constexpr uint32_t kSrcRoot = 16u;       // the src trie root follows the 16-word blob header
 constexpr uint32_t kWalkKeyLimit = 0x30000u;  // keys >= this (ANY protocol) take the linear path

@@ -335,19 +335,21 @@ struct TabEval {
 // Fixed-depth trie lookups (DevNode: leaves point at their class's self word, which points
 // at itself), in lockstep and without per-lane branches: the root read (stride s1 over a W-bit
 // address), then depth - 1 steps of one bit-field extract and one shifted add each (blobwalk.hpp
-// node_child_byte); the class is the self word's index. PRED is unused (kept for the callers).
+// node_child_byte) at a per-level bit offset; the class is the self word's index (e >> 7). PRED
+// is unused (kept for the callers).
 template <bool PRED, class L, int Q>
 PG_HD void node_trie_q(const L& ld, uint32_t root, uint32_t s1, uint32_t W, uint32_t depth, uint32_t self0,
                        const uint32_t (&a)[Q], uint32_t (&c)[Q]) {
-    uint32_t e[Q];
+    uint32_t e[Q], rem = W - s1;
     PG_UNROLL
     for (int j = 0; j < Q; j++) e[j] = ld.u32(root + (a[j] >> (W - s1)));
     for (uint32_t l = 1; l < depth; l++) {
+        rem = node_next_shift(rem);
         PG_UNROLL
-        for (int j = 0; j < Q; j++) e[j] = ld.at_byte(node_child_byte(e[j], a[j]));
+        for (int j = 0; j < Q; j++) e[j] = ld.at_byte(node_child_byte(e[j], a[j], rem));
     }
     PG_UNROLL
-    for (int j = 0; j < Q; j++) c[j] = (e[j] >> 12) - self0;
+    for (int j = 0; j < Q; j++) c[j] = (e[j] >> 7) - self0;
 }
 
 // The IPv4 trie (addresses a) and the L4-key trie (keys b) in one lockstep loop: independent
@@ -355,30 +357,34 @@ PG_HD void node_trie_q(const L& ld, uint32_t root, uint32_t s1, uint32_t W, uint
 template <bool PRED, class L, int QA, int QB>
 PG_HD void node_trie2_q(const L& ld, const DevNode& N, const uint32_t (&a)[QA], uint32_t (&ca)[QA],
                         const uint32_t (&b)[QB], uint32_t (&cb)[QB]) {
-    uint32_t ea[QA], eb[QB];
+    uint32_t ea[QA], eb[QB], ra = 32u - N.ip_s1, rb = 18u - N.key_k1;
     PG_UNROLL
     for (int j = 0; j < QA; j++) ea[j] = ld.u32(a[j] >> (32u - N.ip_s1));
     PG_UNROLL
     for (int j = 0; j < QB; j++) eb[j] = ld.u32(N.key_root + (b[j] >> (18u - N.key_k1)));
     const uint32_t dmin = N.ip_depth < N.key_depth ? N.ip_depth : N.key_depth;
     for (uint32_t l = 1; l < dmin; l++) {
+        ra = node_next_shift(ra);
+        rb = node_next_shift(rb);
         PG_UNROLL
-        for (int j = 0; j < QA; j++) ea[j] = ld.at_byte(node_child_byte(ea[j], a[j]));
+        for (int j = 0; j < QA; j++) ea[j] = ld.at_byte(node_child_byte(ea[j], a[j], ra));
         PG_UNROLL
-        for (int j = 0; j < QB; j++) eb[j] = ld.at_byte(node_child_byte(eb[j], b[j]));
+        for (int j = 0; j < QB; j++) eb[j] = ld.at_byte(node_child_byte(eb[j], b[j], rb));
     }
     for (uint32_t l = dmin; l < N.ip_depth; l++) {
+        ra = node_next_shift(ra);
         PG_UNROLL
-        for (int j = 0; j < QA; j++) ea[j] = ld.at_byte(node_child_byte(ea[j], a[j]));
+        for (int j = 0; j < QA; j++) ea[j] = ld.at_byte(node_child_byte(ea[j], a[j], ra));
     }
     for (uint32_t l = dmin; l < N.key_depth; l++) {
+        rb = node_next_shift(rb);
         PG_UNROLL
-        for (int j = 0; j < QB; j++) eb[j] = ld.at_byte(node_child_byte(eb[j], b[j]));
+        for (int j = 0; j < QB; j++) eb[j] = ld.at_byte(node_child_byte(eb[j], b[j], rb));
     }
     PG_UNROLL
-    for (int j = 0; j < QA; j++) ca[j] = (ea[j] >> 12) - N.ipself;
+    for (int j = 0; j < QA; j++) ca[j] = (ea[j] >> 7) - N.ipself;
     PG_UNROLL
-    for (int j = 0; j < QB; j++) cb[j] = (eb[j] >> 12) - N.kself;
+    for (int j = 0; j < QB; j++) cb[j] = (eb[j] >> 7) - N.kself;
 }
 
 #ifndef PG_NODE_WALK2  // node kernels: IPv4 and key tries in one lockstep walk

@@ -140,7 +140,6 @@ struct Tuning {
     uint32_t pair = 1;             // PAIR for tables CROSS cannot take (0 = CAND, 2 = wherever it fits)
     uint32_t node_build = 1;       // build the node classifier (PERPOD / CONN)
     uint32_t node_root_bits = 12;  // its IPv4 / key trie root stride cap (4..16)
-    uint32_t lc_node = 0;          // level-compressed node IPv4 trie
     uint32_t node_common = 1;      // common-row section of node images
     uint32_t fd = 1;               // FD form of dst-independent CROSS tables that fit LDS
     uint32_t candi = 1;            // CANDI form (inline candidates) of dst-independent HBM-resident CAND tables

@@ -33,7 +33,6 @@ const Knob kKnobs[] = {
     {"pair", &Tuning::pair, 0, 2, true},
     {"node_build", &Tuning::node_build, 0, 1, true},
     {"node_root_bits", &Tuning::node_root_bits, 4, 16, true},
-    {"lc_node", &Tuning::lc_node, 0, 1, true},
     {"node_common", &Tuning::node_common, 0, 1, true},
     {"fd", &Tuning::fd, 0, 1, true},
     {"candi", &Tuning::candi, 0, 1, true},

@@ -73,9 +73,9 @@ constexpr uint32_t kTrieFail = 0xFFFFFFFFu;
 // (default 12: 16 KiB per workgroup; A/B on MI355X, config 4: 163 Gpps at 12 vs 131 at 14 --
 // the 64 KiB root of 14 bits held the launch to half the resident waves)
 // enc: kEncBlob (blobwalk.hpp trie_child / trie_stride); kEncNode, the node image's encoding
-// (blobwalk.hpp node_child): a non-leaf entry holds the child's BYTE offset << 10 | stride << 5
-// | the address shift of the child level, so a step is one bit-field extract and one shifted
-// add, children below 2 MiB; kEncWords, the FD blobs' (blobwalk.hpp fd_walk): the same with
+// (blobwalk.hpp node_child_byte): a non-leaf entry holds the child's BYTE offset << 5 | stride,
+// the levels below the root take uniform strides (the bit offset of a level is a per-level
+// constant), so a step is one bit-field extract and one shifted add; kEncWords, the FD blobs' (blobwalk.hpp fd_walk): the same with
 // the child's WORD offset, children below 16 MiB.
 enum TrieEnc { kEncBlob = 0, kEncNode = 1, kEncWords = 2 };
 constexpr uint32_t kWordsChildMax = 1u << 22;
@@ -123,7 +123,7 @@ uint32_t build_trie(std::vector<uint32_t>& blob, const std::vector<uint64_t>& bn
             const uint64_t lim = enc == kEncNode ? kNodeChildMaxWords : (enc == kEncWords ? kWordsChildMax : kTrieChildMask);
             if ((uint64_t)child + (1ull << st) > lim) return kTrieFail;
             blob.resize(blob.size() + (1u << st), 0);
-            blob[j.block + e] = enc == kEncNode    ? node_entry(child, st, j.shift - st)
+            blob[j.block + e] = enc == kEncNode    ? node_entry(child, st)
                                 : enc == kEncWords ? (child << 10 | st << 5 | (j.shift - st))
                                                    : child | (st << kTrieStrideShift);
             stack.push_back({child, a, j.shift - st, st});
@@ -679,7 +679,7 @@ bool build_fast_table(const DevRule* rules, uint32_t n, uint32_t rule_base, uint
     return true;
 }
 
-// ---- node tries: depth and fixed-depth leaves (kEncNode: child BYTE offset << 10) -------------
+// ---- node tries: depth and fixed-depth leaves (kEncNode: child BYTE offset << 5) --------------
 namespace {
 uint32_t node_trie_depth(const std::vector<uint32_t>& b, uint32_t root, uint32_t s1) {
     uint32_t d = 1;
@@ -694,7 +694,7 @@ uint32_t node_trie_depth(const std::vector<uint32_t>& b, uint32_t root, uint32_t
         for (uint32_t e = 0; e < j.n; e++) {
             const uint32_t v = b[j.at + e];
             if (v & kLeaf) continue;
-            st.push_back({(v >> 10) / 4u, 1u << ((v >> 5) & 31u), j.depth + 1});
+            st.push_back({(v >> 5) / 4u, 1u << (v & 31u), j.depth + 1});
         }
     }
     return d;
@@ -707,8 +707,8 @@ void node_point_leaves(std::vector<uint32_t>& b, uint32_t root, uint32_t s1, uin
         st.pop_back();
         for (uint32_t e = 0; e < j.second; e++) {
             uint32_t& v = b[j.first + e];
-            if (v & kLeaf) v = ((self0 + (v & ~kLeaf)) * 4u) << 10;
-            else st.push_back({(v >> 10) / 4u, 1u << ((v >> 5) & 31u)});
+            if (v & kLeaf) v = ((self0 + (v & ~kLeaf)) * 4u) << 5;
+            else st.push_back({(v >> 5) / 4u, 1u << (v & 31u)});
         }
     }
 }
@@ -994,7 +994,7 @@ bool build_node(HostTableSet& h, const std::vector<TableAnalysis*>& an, const st
         std::vector<uint32_t> tmp;
         for (uint32_t s1 = top; s1 + 4 > top && s1 >= 4; s1--) {
             tmp.clear();
-            if (build_trie(tmp, gb, gcls, 32, s1, tu, tu.lc_node != 0, kEncNode) != 0) return false;
+            if (build_trie(tmp, gb, gcls, 32, s1, tu, false, kEncNode, kNodeStride) != 0) return false;
             const uint32_t d = node_trie_depth(tmp, 0, s1);
             if (d < best_d || (d == best_d && tmp.size() < img.size())) {
                 best_d = d;
@@ -1004,15 +1004,15 @@ bool build_node(HostTableSet& h, const std::vector<TableAnalysis*>& an, const st
         }
     }
     N.key_k1 = std::min(pick_stride(kb.size(), 18, tu), tu.node_root_bits);
-    N.key_root = build_trie(img, kb, kcls, 18, N.key_k1, tu, false, kEncNode);
+    N.key_root = build_trie(img, kb, kcls, 18, N.key_k1, tu, false, kEncNode, kNodeStride);
     if (N.key_root == kTrieFail) return false;
     // fixed depth: leaves -> self words of their classes (DevNode)
     N.ip_depth = node_trie_depth(img, 0, N.ip_s1);
     N.key_depth = node_trie_depth(img, N.key_root, N.key_k1);
     N.ipself = (uint32_t)img.size();
-    for (uint32_t g = 0; g < G; g++) img.push_back(((N.ipself + g) * 4u) << 10);
+    for (uint32_t g = 0; g < G; g++) img.push_back(((N.ipself + g) * 4u) << 5);
     N.kself = (uint32_t)img.size();
-    for (uint32_t g = 0; g < GK; g++) img.push_back(((N.kself + g) * 4u) << 10);
+    for (uint32_t g = 0; g < GK; g++) img.push_back(((N.kself + g) * 4u) << 5);
     if ((uint64_t)img.size() * 4 >= kNodeChildMaxWords * 4ull) return false;
     node_point_leaves(img, 0, N.ip_s1, N.ipself);
     node_point_leaves(img, N.key_root, N.key_k1, N.kself);
