@@ -236,7 +236,8 @@ PG_HD void probe_q(const DevTableSet& T, const uint32_t (&ip)[Q], End (&e)[Q]) {
 
 // per-rule hit counters: LDS histogram (u32) or global u64 slots on the device, plain u64
 // slots on the host
-struct Hist {
+template <bool kFullLds = false>  // true: lds (when set) holds every slot (node kernels)
+struct HistT {
     uint32_t* lds;
     unsigned long long* glob;
     // device, lds set: cells [0, wn) count slots [wbase, wbase + wn), cells wn and wn + 1 count
@@ -271,7 +272,7 @@ struct Hist {
         }
         if (!done) {
             const uint32_t c = slot - wbase;
-            if (lds && full) atomicAdd(&lds[slot], 1u);
+            if (lds && (kFullLds || full)) atomicAdd(&lds[slot], 1u);
             else if (lds && c < wn) atomicAdd(&lds[c], 1u);
             else if (lds && slot == xslot) atomicAdd(&lds[wn], 1u);
             else if (lds && slot == xslot1) atomicAdd(&lds[wn + 1], 1u);
@@ -282,6 +283,7 @@ struct Hist {
 #endif
     }
 };
+using Hist = HistT<false>;
 
 // SINGLE mode over an FD table (uniform: tab0): Q tuples per lane, fixed-depth walks in
 // lockstep; ANY-protocol packets take the linear scan. prefix: the blob's prefix (its LDS copy
@@ -566,9 +568,9 @@ struct NodeEval {
 };
 
 // one evalACL step of testConnection / per-pod mode: tables t[j] (-1 = no ACL: PERMIT)
-template <int Q, bool COUNT, class EV>
+template <int Q, bool COUNT, class EV, class HS>
 PG_HD void eval_step(const DevTableSet& T, const EV& ev, const int32_t (&t)[Q], const bool (&run)[Q], bool rev,
-                     const Hist& h, uint32_t (&w)[Q]) {
+                     const HS& h, uint32_t (&w)[Q]) {
     bool act[Q];
     PG_UNROLL
     for (int j = 0; j < Q; j++) {
@@ -585,8 +587,8 @@ PG_HD void eval_step(const DevTableSet& T, const EV& ev, const int32_t (&t)[Q], 
 
 // testConnection (aclengine_mock.go:424-501) of Q connections on resolved end points, each
 // of its up-to-4 evalACL steps in lockstep over the Q connections.
-template <int Q, bool COUNT, class EV>
-PG_HD void conn_q(const DevTableSet& T, const EV& ev, const End (&es)[Q], const End (&ed)[Q], const Hist& h,
+template <int Q, bool COUNT, class EV, class HS>
+PG_HD void conn_q(const DevTableSet& T, const EV& ev, const End (&es)[Q], const End (&ed)[Q], const HS& h,
                   uint32_t (&out)[Q]) {
     bool live[Q], srefl[Q], drefl[Q], same[Q], run[Q];
     uint32_t w[Q];
@@ -712,10 +714,10 @@ PG_HD void classify_q(const DevTableSet& T, const uint32_t* blobs, const DevTabl
 
 // Q tuples of one lane, PERPOD / CONN, node path. `img` reads the node image (LDS copy or
 // global memory).
-template <int MODE, bool COUNT, int Q, bool PRED = false, bool CM = false, class L, class H = NoHook>
+template <int MODE, bool COUNT, int Q, bool PRED = false, bool CM = false, class L, class HS, class H = NoHook>
 PG_HD void classify_node_q(const DevTableSet& T, const DevNode& N, const L& img, const uint32_t (&s)[Q],
                            const uint32_t (&d)[Q], const uint32_t (&sp)[Q], const uint32_t (&dp)[Q],
-                           const uint32_t (&pr)[Q], const Hist& h, uint32_t (&out)[Q], const H& hook = H()) {
+                           const uint32_t (&pr)[Q], const HS& h, uint32_t (&out)[Q], const H& hook = H()) {
     uint32_t key[Q], kack[Q];
     PG_UNROLL
     for (int j = 0; j < Q; j++) key[j] = pkt_key(pr[j], dp[j]), kack[j] = MODE == 2 ? pkt_key(pr[j], sp[j]) : key[j];

@@ -461,7 +461,8 @@ void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
     constexpr bool NODST = MODE == 0 && STAGE_ >= 8;
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     uint32_t* hist = smem + (STAGE ? stage_words : 0u);
-    Hist h{nullptr, counters};
+    // node kernels: the LDS histogram, when used, holds every slot (HistT<true>: no window test)
+    HistT<NODE> h{nullptr, counters};
     DevTable tab0{};
     const uint32_t* blobs = T.blobs;
     // the node image: its LDS copy (at LDS address 0: LdsLoader) when staged, else global memory
@@ -492,13 +493,15 @@ void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
     // favours them: config 4's Zipf depth) and the extra cells its default-deny slot and its
     // last rule (a deny-the-rest / allow-all catch-all takes every unmatched packet: a single
     // global address would serialise them); node modes: "no ACL", "unresolved"
+    // node kernels over more slots than the histogram holds count with global atomics only
+    const bool lds_hist = COUNT && (!NODE || hist_cells >= T.n_slots);
     const uint32_t wn = COUNT ? hist_cells : 0u;
     const uint32_t wbase = (MODE == 0 && wn < T.n_slots) ? min(tab0.rule_base, T.n_slots - wn) : 0u;
     const uint32_t xslot = MODE == 0 ? (tab0.dflt & kSlotMask) : T.slot_noacl;
     const uint32_t xslot1 = MODE == 0 ? (tab0.n_rules ? tab0.rule_base + tab0.n_rules - 1u : xslot) : T.slot_unresolved;
     if (COUNT) {
         for (uint32_t i = threadIdx.x; i <= wn + 1u; i += BS) hist[i] = 0;
-        h.lds = hist;
+        h.lds = lds_hist ? hist : nullptr;
         h.wbase = wbase;
         h.wn = wn;
         h.xslot = xslot;
