@@ -1,8 +1,8 @@
 #!/usr/bin/env python3
 """Measurement tool: per-launch time of back-to-back classify launches (config 2) -- plain
 launches, and the same launches replayed from a captured graph -- to size the inter-kernel gap
-(DESIGN.md §5). PG_PROBE_SKIP_MARK=1 in the environment skips the per-launch use-event record
-(measurement only: the table set's safe-free bookkeeping is then off)."""
+(DESIGN.md §4 "Completion events": measured with a temporary build that skipped the per-launch
+use-event record, 130.2 -> 127.1 us per config-2 launch, before the fence-free events)."""
 import os
 import sys
 
@@ -44,8 +44,7 @@ def main():
                 D.classify(e, w.mode, w.table_id, b, out)
     torch.cuda.current_stream().wait_stream(s)
     graph = timed(lambda: g.replay())
-    print({"launches": k, "skip_mark": bool(os.environ.get("PG_PROBE_SKIP_MARK")),
-           "plain_us_per_launch": round(plain * 1e3 / k, 2), "graph_us_per_launch": round(graph * 1e3 / k, 2)})
+    print({"launches": k, "plain_us_per_launch": round(plain * 1e3 / k, 2), "graph_us_per_launch": round(graph * 1e3 / k, 2)})
 
 
 if __name__ == "__main__":

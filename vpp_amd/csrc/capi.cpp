@@ -745,10 +745,9 @@ int pg_classify(pg_ctx* ctx, int mode, int table_id, const pg_tuple_soa* t, uint
     if (!t->src_ip || !t->dst_ip || !t->dst_port || !t->proto || (mode == PG_MODE_CONN && !t->src_port))
         return fail(ctx, PG_EINVAL, "missing tuple field");
     std::string err;
-    static const bool skip_mark = std::getenv("PG_PROBE_SKIP_MARK") != nullptr;  // measurement aid only
     if (dev_classify(T, ctx->eng.tune, mode, table_id, t->src_ip, t->dst_ip, t->src_port, t->dst_port, t->proto, n,
                      out, (unsigned long long*)counters, stream, &err) != 0 ||
-        (!skip_mark && dev_mark_use(ctx->eng.cur, stream, counters != nullptr, &err) != 0))
+        dev_mark_use(ctx->eng.cur, stream, counters != nullptr, &err) != 0)
         return fail(ctx, PG_EIO, err);
     return PG_OK;
     GUARD_END(ctx)
