@@ -830,9 +830,13 @@ static void launch_bs(const DevTableSet& T, const Tuning& tu, int t, const uint3
                       const uint16_t* dport, const uint8_t* proto, uint64_t n, uint32_t* out,
                       unsigned long long* counters, hipStream_t st, size_t hist, uint32_t stage, uint64_t items) {
     auto k = k_classify<MODE, COUNT, VEC, STAGE, NODE, BS>;
+    // SINGLE over an LDS-staged FD table without counters: two resident workgroups per CU, not
+    // the three LDS would allow (A/B on MI355X, config 2: 541-546 vs 533-535 Gpps, repeated
+    // three times; with counters no difference): fewer streams in flight per CU contend less
+    const uint32_t bpc = tu.blocks_per_cu ? tu.blocks_per_cu : (MODE == 0 && (STAGE & 7) == 4 && !COUNT ? 2u : 0u);
     const size_t lds = hist + (size_t)stage * 4;
     const uint32_t cells = hist ? (uint32_t)(hist / 4 - 2) : 0u;  // window cells (+ the two extra ones)
-    hipLaunchKernelGGL(k, dim3(grid_resident(k, BS, lds, items, tu.blocks_per_cu)), dim3(BS), lds, st, T, t, src, dst, sport, dport,
+    hipLaunchKernelGGL(k, dim3(grid_resident(k, BS, lds, items, bpc)), dim3(BS), lds, st, T, t, src, dst, sport, dport,
                        proto, n, out, counters, stage, cells);
 }
 
