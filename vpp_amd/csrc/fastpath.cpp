@@ -23,7 +23,8 @@
 //
 // Blob words (u32), all offsets relative to the blob start so it can be read from HBM or
 // copied verbatim into LDS:
-//   [0]  flags: 1 = CROSS, 2 = LISTS, 4 = CAND, 16 = PAIR
+//   [0]  flags: 1 = CROSS, 2 = LISTS, 4 = CAND, 16 = PAIR, 32 = FD (build_fd_blob), 128 = CANDI
+//        (candidates inline in 8-B trie entries below the root; build_fast_table CANDI section)
 //   [1]  default verdict (DENY << 30 | table's default slot)
 //   [2]  src trie root (always 16)   [3] s1     [4] key trie root   [5] k1
 //   [6]  CROSS: cross table (u32 verdicts, or LISTS: u2 {verdict, first record | 0});
@@ -31,8 +32,10 @@
 //   [7]  n_key_classes   [10] n_src_classes   [8, 9, 11] reserved
 //   PAIR (flag 16): [6] pair x key verdicts, [12] dst trie root, [13] d1, [14] (src class x
 //        dst class) -> pair class table, [15] n_dst_classes
-//   records (16 B, blobwalk.hpp): {dnet, klo | dst prefix length << 18, khi, verdict}; every
-//   list ends with a match-all record carrying the fall-through verdict.
+//   records (16 B, blobwalk.hpp): {dnet, klo | dst prefix length << 18 | last << 24, khi,
+//   verdict}; a dst list (LISTS, node lists) ends with a match-all record carrying the
+//   fall-through verdict, a candidate list (CAND, CANDI) flags its last record instead (no
+//   match there: the table's default deny; an empty list is one match-all record carrying it).
 #include <algorithm>
 #include <map>
 #include <set>
