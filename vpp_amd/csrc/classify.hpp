@@ -244,10 +244,19 @@ struct HistT {
     // slots xslot and xslot1, other slots go to glob (device.hip k_classify)
     uint32_t wbase = 0, wn = 0xFFFFFFFFu, xslot = 0xFFFFFFFFu, xslot1 = 0xFFFFFFFFu;
     bool full = true;  // the window holds every slot (wave-uniform: the common case costs no test)
+    // SINGLE kernels: slot `hot` (the table's last rule: a catch-all takes every unmatched
+    // packet) counted per lane in a register and added once at the end (flush_hot) -- many
+    // lanes of a wave on one LDS address serialise their atomics
+    uint32_t hot = 0xFFFFFFFFu;
+    mutable uint32_t nhot = 0;
     PG_HD void inc(uint32_t slot) const {
 #if defined(__HIP_DEVICE_COMPILE__) && defined(PG_PROBE_NOINC)  // measurement build only
         if (slot == 0xFFFFFFFFu) lds[0] = 0;
 #elif defined(__HIP_DEVICE_COMPILE__)
+        if (slot == hot) {
+            nhot++;
+            return;
+        }
         // One LDS (or global) atomic per lane. PG_AGG_ROUNDS > 0 first lets the lanes that
         // share the first active lane's slot (a reflective ACL's rule, "no ACL", a default
         // deny) add their count with one atomic, per round; A/B on MI355X with warmed-up
@@ -280,6 +289,21 @@ struct HistT {
         }
 #else
         if (glob) glob[slot]++;
+#endif
+    }
+    PG_HD void flush_hot() const {  // device: the register count of `hot` into the histogram
+#if defined(__HIP_DEVICE_COMPILE__)
+        if (nhot) {
+            const uint32_t h0 = hot;
+            const uint32_t n = nhot;
+            nhot = 0;
+            const uint32_t c = h0 - wbase;
+            if (lds && (kFullLds || full)) atomicAdd(&lds[h0], n);
+            else if (lds && c < wn) atomicAdd(&lds[c], n);
+            else if (lds && h0 == xslot) atomicAdd(&lds[wn], n);
+            else if (lds && h0 == xslot1) atomicAdd(&lds[wn + 1], n);
+            else if (glob) atomicAdd(&glob[h0], (unsigned long long)n);
+        }
 #endif
     }
 };

@@ -438,6 +438,9 @@ __device__ __forceinline__ void st_words(const Words<NW>& v, uint32_t* p) {
 #endif
 // SINGLE over a blob in HBM (STAGE 0 / 2, the dst-free variants included): 66 registers at four
 // tuples per chunk hold it to three 512-thread workgroups per CU; a 64-register cap spills
+#ifndef PG_HOT_SLOT  // SINGLE with counters: the table's last rule counted in a register (HistT::hot)
+#define PG_HOT_SLOT 1
+#endif
 #ifndef PG_SINGLE_HBM_WPE  // (A/B on MI355X, config 4: 8 = 164.6 Gpps with 2 spills, 1 = 175.7)
 #define PG_SINGLE_HBM_WPE 1
 #endif
@@ -507,6 +510,7 @@ void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
         h.xslot = xslot;
         h.xslot1 = xslot1;
         h.full = wn >= T.n_slots;
+        if (MODE == 0 && PG_HOT_SLOT) h.hot = xslot1;
     }
     if (STAGE || COUNT) __syncthreads();
     const uint64_t stride = (uint64_t)gridDim.x * BS;
@@ -615,6 +619,7 @@ void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
         out[i] = o[0];
     }
     if (COUNT) {
+        h.flush_hot();
         __syncthreads();
         for (uint32_t i = threadIdx.x; i <= wn + 1u; i += BS) {
             const uint32_t v = hist[i];
