@@ -441,6 +441,9 @@ __device__ __forceinline__ void st_words(const Words<NW>& v, uint32_t* p) {
 #ifndef PG_HOT_SLOT  // SINGLE with counters: the table's last rule counted in a register (HistT::hot)
 #define PG_HOT_SLOT 1
 #endif
+#ifndef PG_HOT_SLOT_NODE  // node kernels with counters: the node-output table's last rule in a register
+#define PG_HOT_SLOT_NODE 1
+#endif
 #ifndef PG_SINGLE_HBM_WPE  // (A/B on MI355X, config 4: 8 = 164.6 Gpps with 2 spills, 1 = 175.7)
 #define PG_SINGLE_HBM_WPE 1
 #endif
@@ -511,6 +514,14 @@ void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
         h.xslot1 = xslot1;
         h.full = wn >= T.n_slots;
         if (MODE == 0 && PG_HOT_SLOT) h.hot = xslot1;
+        // node kernels whose table set has more slots than the LDS histogram holds (every
+        // increment a global atomic): the catch-all of the node-output interface's outbound
+        // table (traffic to remote pods and the Internet) in a register -- config 6 with
+        // counters 0.4 -> 5.6 Gpps; with the histogram in LDS it costs 2 % (configs 3, 5)
+        if (MODE != 0 && PG_HOT_SLOT_NODE && !lds_hist && T.node_out >= 0) {
+            const DevTable no = load_tab(T.tabs, T.node_out);
+            if (no.n_rules) h.hot = no.rule_base + no.n_rules - 1u;
+        }
     }
     if (STAGE || COUNT) __syncthreads();
     const uint64_t stride = (uint64_t)gridDim.x * BS;
