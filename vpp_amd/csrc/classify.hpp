@@ -236,7 +236,9 @@ PG_HD void probe_q(const DevTableSet& T, const uint32_t (&ip)[Q], End (&e)[Q]) {
 
 // per-rule hit counters: LDS histogram (u32) or global u64 slots on the device, plain u64
 // slots on the host
-template <bool kFullLds = false>  // true: lds (when set) holds every slot (node kernels)
+// kFullLds: lds (when set) holds every slot (node kernels); kAggGlobal: with lds unset, global
+// increments are aggregated per distinct slot over the wave (PERPOD node kernels)
+template <bool kFullLds = false, bool kAggGlobal = false>
 struct HistT {
     uint32_t* lds;
     unsigned long long* glob;
@@ -281,11 +283,31 @@ struct HistT {
         }
         if (!done) {
             const uint32_t c = slot - wbase;
+            bool g = false;
             if (lds && (kFullLds || full)) atomicAdd(&lds[slot], 1u);
             else if (lds && c < wn) atomicAdd(&lds[c], 1u);
             else if (lds && slot == xslot) atomicAdd(&lds[wn], 1u);
             else if (lds && slot == xslot1) atomicAdd(&lds[wn + 1], 1u);
-            else if (glob) atomicAdd(&glob[slot], 1ull);
+            else g = glob != nullptr;
+            if (g && !(kAggGlobal && !lds)) {
+                atomicAdd(&glob[slot], 1ull);
+            } else if (g) {
+                // PERPOD node kernels over a table set larger than the LDS histogram (every
+                // increment a global atomic): aggregated per distinct slot over the wave's lanes,
+                // one atomic per slot instead of one per lane -- the per-table catch-alls
+                // serialise at the L2 otherwise (config 6 with counters 5.6 -> 8.3 Gpps; on
+                // SINGLE's windowed histogram, whose global slots are mostly distinct, the loop
+                // cost 3-11 %; in the register-capped CONN kernel its code cost 2.5 %)
+                for (;;) {
+                    const uint32_t lead = __builtin_amdgcn_readfirstlane(slot);
+                    const unsigned long long m = __ballot(slot == lead);
+                    if (slot == lead) {
+                        if (__lane_id() == (unsigned)(__ffsll((long long)m) - 1))
+                            atomicAdd(&glob[lead], (unsigned long long)__popcll(m));
+                        break;
+                    }
+                }
+            }
         }
 #else
         if (glob) glob[slot]++;

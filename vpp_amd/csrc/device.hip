@@ -468,7 +468,7 @@ void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     uint32_t* hist = smem + (STAGE ? stage_words : 0u);
     // node kernels: the LDS histogram, when used, holds every slot (HistT<true>: no window test)
-    HistT<NODE> h{nullptr, counters};
+    HistT<NODE, NODE && MODE == 1> h{nullptr, counters};
     DevTable tab0{};
     const uint32_t* blobs = T.blobs;
     // the node image: its LDS copy (at LDS address 0: LdsLoader) when staged, else global memory
