@@ -284,7 +284,11 @@ struct HistT {
         if (!done) {
             const uint32_t c = slot - wbase;
             bool g = false;
+#if defined(PG_PROBE_PLAINST)  // measurement build only: a plain LDS store in place of the atomic
+            if (lds && (kFullLds || full)) lds[slot] = 1u;
+#else
             if (lds && (kFullLds || full)) atomicAdd(&lds[slot], 1u);
+#endif
             else if (lds && c < wn) atomicAdd(&lds[c], 1u);
             else if (lds && slot == xslot) atomicAdd(&lds[wn], 1u);
             else if (lds && slot == xslot1) atomicAdd(&lds[wn + 1], 1u);
