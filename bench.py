@@ -54,6 +54,9 @@ def parse():
     p.add_argument("--faithful-seconds", type=float, default=8.0,
                    help="budget of the single-thread reference-faithful CPU variant (SINGLE mode)")
     p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--check-tuples", type=int, default=1 << 20,
+                   help="tuples of every rank's shard checked against the oracle after the timed region")
+    p.add_argument("--no-check", action="store_true", help="skip the per-rank oracle self-check")
     p.add_argument("--per-table", action="store_true",
                    help="PERPOD/CONN through the per-table blobs + IP hash instead of the node classifier")
     p.add_argument("--cpu-dry-run", action="store_true",
@@ -154,12 +157,6 @@ def main():
     total_tuples = VD.sum_over_ranks(n, "cuda") * a.steps
     mpps = total_tuples / wall / 1e6
 
-    # statscollector path: the per-rule hit counters of one counted pass over every rank's
-    # shard, summed by RCCL through the library's own communicator (pg_allreduce_counters)
-    allreduce = None
-    if launched:
-        allreduce = counter_allreduce(e, w, b, out, rank, world)
-
     bpt, fields = bytes_per_tuple(w)
     achieved = n * bpt / (kern_ms * 1e-3) / 1e9
     traffic, traffic_src = pmc_traffic(a.config, n, (a.counters and not w.counters) or bool(a.rules))
@@ -177,8 +174,6 @@ def main():
                      "bytes_per_tuple": bpt, "fields": fields, "kernel_ms": round(kern_ms, 4),
                      "algorithmic_bytes_per_launch": n * bpt, "traffic_source": traffic_src},
     }
-    if allreduce is not None:
-        line.update(allreduce)
     # the same fraction against what moving this launch's own bytes reaches on this GPU (after
     # the timed region): pg_stream_probe issues the classify launch's loads and store over the
     # same batch without the classification; torch's 1 GiB device copy beside it
@@ -186,9 +181,28 @@ def main():
     cp = torch_copy_gbps()
     line["roofline"]["measured_stream_gbps"] = {"probe": probe, "copy": cp}
     line["roofline"]["frac_of_measured_stream"] = round(achieved / probe, 4)
+
+    # Self-check of every rank's shard (after the timed region), whatever the world size: the
+    # timed run's verdicts of the shard's first --check-tuples tuples against the oracle, and a
+    # counted pass over them whose hit counters must equal the oracle's histogram
+    check_threads = max(1, host_cores() // world)
+    par = shard_check(w, b, out, base, a.check_tuples, check_threads) if not a.no_check else None
+    # statscollector path (torchrun launches): the per-rule hit counters of one counted pass over
+    # every rank's whole shard, summed by RCCL through the library's own communicator
+    # (pg_allreduce_counters) and checked against torch.distributed's sum of the same local
+    # histograms
+    if launched:
+        line.update(counter_allreduce(e, w, b, out, rank, world))
+    if par is not None:
+        pars = VD.gather_objects(par)
+        line["parity_sample"] = {"ranks": world, "tuples": sum(p["tuples"] for p in pars),
+                                 "bit_exact_action_and_rule_index": all(p["bit_exact_action_and_rule_index"]
+                                                                        for p in pars),
+                                 "counters_equal_oracle_histogram": all(p["counters_equal_oracle_histogram"]
+                                                                        for p in pars)}
+        line["parity_per_rank"] = pars
     if rank == 0 and world == 1 and not a.no_cpu:
-        line["cpu_baseline"], line["parity_sample"] = cpu_baseline(w, b, out, a.cpu_sample, a.faithful_seconds,
-                                                                   a.cpu_seconds)
+        line["cpu_baseline"] = cpu_baseline(w, b, out, a.cpu_sample, a.faithful_seconds, a.cpu_seconds)
     if rank == 0:
         print(json.dumps(line), file=json_out, flush=True)
     if launched:
@@ -196,10 +210,12 @@ def main():
 
 
 def counter_allreduce(e, w, b, out, rank, world):
-    """One counted classify pass per rank into the context's own counters, then
-    pg_allreduce_counters over an RCCL communicator the library holds (unique id from rank 0
-    over torch.distributed). Returns the timing and a consistency check: every tuple of every
-    rank is counted (SINGLE / PERPOD: one evaluation per tuple; CONN: at least one)."""
+    """One counted classify pass per rank over its whole shard into the context's own
+    counters, then pg_allreduce_counters over an RCCL communicator the library holds (unique id
+    from rank 0 over torch.distributed). Checked (every rank): SINGLE / PERPOD local counters
+    == the histogram of the pass's verdict slots (one evaluation per tuple); the RCCL sum ==
+    torch.distributed's all_reduce of the same local histograms; the local counters unchanged
+    by the reduction; SINGLE / PERPOD sum == every tuple of every rank."""
     res = {}
     try:
         uid = [D.comm_unique_id() if rank == 0 else None]
@@ -208,25 +224,67 @@ def counter_allreduce(e, w, b, out, rank, world):
         D.reset_counters(e)
         D.classify(e, w.mode, w.table_id, b, out, counters=D.counters_device_ptr(e))
         torch.cuda.synchronize()
+        local = D.read_counters(e).astype(np.int64)
+        checks = {}
+        if w.mode != 2:
+            h = torch.bincount((out & 0x3FFFFFFF).long(), minlength=len(local)).cpu().numpy()
+            checks["local_equals_verdict_histogram"] = bool(np.array_equal(h, local))
         dist.barrier()
         t1 = time.perf_counter()
-        summed = D.allreduce_counters(e)
+        summed = D.allreduce_counters(e).astype(np.int64)
         res["counter_allreduce_ms"] = round((time.perf_counter() - t1) * 1e3, 3)
+        ref = torch.from_numpy(local).cuda()
+        dist.all_reduce(ref)
+        checks["rccl_sum_equals_torch_sum"] = bool(np.array_equal(summed, ref.cpu().numpy()))
+        checks["local_unchanged_by_reduction"] = bool(np.array_equal(D.read_counters(e).astype(np.int64), local))
         total = VD.sum_over_ranks(b.n, "cuda")
-        got = int(summed.sum())
-        res["counter_allreduce_check"] = bool(got == total if w.mode != 2 else got >= total)
+        checks["sum_accounts_for_every_tuple"] = bool(int(summed.sum()) == total if w.mode != 2
+                                                      else int(summed.sum()) >= total)
+        per_rank = VD.gather_objects(checks)
+        res["counter_allreduce_check"] = all(all(c.values()) for c in per_rank)
+        res["counter_allreduce_checks_per_rank"] = per_rank
         res["counter_slots"] = int(len(summed))
+        res["counter_evaluations_total"] = int(summed.sum())
     except Exception as ex:  # reported, not fatal: the throughput line still prints
         res["counter_allreduce_error"] = str(ex)[:300]
+        res["counter_allreduce_check"] = False
     return res
+
+
+def shard_check(w, b, out, base, k, threads):
+    """Self-check of this rank's shard (after the timed region; the oracle is the checker, never
+    the thing measured): the timed run's verdicts of the shard's first k tuples (global indices
+    base .. base + k) against the oracle, bit for bit (action and deciding rule slot), and a
+    counted classify pass over those k tuples whose per-rule hit counters must equal the
+    oracle's histogram -- one count per evalACL, so CONN's up-to-four evaluations per
+    connection are checked too (aclengine_mock.go:448-491)."""
+    from oracle import world as OW  # checker leg
+    e = w.engine
+    k = min(k, b.n)
+    tup = b.numpy(k)
+    got = out[:k].cpu().numpy().view(np.uint32)
+    t0 = time.perf_counter()
+    act, slot, hist = OW.expected(e, w.mode, w.table_id, w.local_ifs, w.node_if, *tup, threads=threads)
+    dt = time.perf_counter() - t0
+    ok = bool(np.array_equal(got >> 30, act.astype(np.uint32)) and np.array_equal(got & 0x3FFFFFFF, slot))
+    sink = torch.empty(k, dtype=torch.int32, device="cuda")
+    D.reset_counters(e)
+    D.classify(e, w.mode, w.table_id, b, sink, counters=D.counters_device_ptr(e), n=k)
+    cnt = D.read_counters(e).astype(np.int64)
+    same = bool(np.array_equal(sink.cpu().numpy().view(np.uint32), got))
+    return {"index_base": int(base), "tuples": int(k), "bit_exact_action_and_rule_index": ok,
+            "counters_equal_oracle_histogram": bool(np.array_equal(cnt, hist)) and same,
+            "evaluations": int(hist.sum()), "oracle_s": round(dt, 2), "oracle_threads": threads}
 
 
 def dry_run(a, rank, world):
     """CPU rehearsal of the multi-rank path (gloo): same launcher, sharding, barriers,
-    max-over-ranks timing and counter all-reduce as on GPUs; the per-tuple code is the
-    product's, run on the host (pg_debug_classify_host); inputs are a numpy restatement of a
-    small random shard. Prints the same JSON line with "dry_run": true."""
-    import numpy as np
+    max-over-ranks timing, per-rank self-check and counter all-reduce as on GPUs; the per-tuple
+    code is the product's, run on the host (pg_debug_classify_host); inputs are the oracle's
+    restatement of the device generator (oracle/gen.py) at the rank's global index range.
+    Prints the same JSON line with "dry_run": true."""
+    from oracle import gen
+    from oracle import world as OW
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     if world > 1:
         dist.init_process_group("gloo")
@@ -236,35 +294,46 @@ def dry_run(a, rank, world):
     w = W.CONFIGS[a.config](0, **kw)
     e = w.engine
     base, n = shard_of(a, w, rank, world)
-    rng = np.random.default_rng([w.gen["seed"], base])
-    src = rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32)
-    dst = rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32)
-    pool = w.gen.get("ip_pool")
-    if pool is not None and len(pool):
-        m = rng.random(n) < 0.8
-        dst[m] = np.asarray(pool, np.uint32)[rng.integers(0, len(pool), int(m.sum()))]
-    sport = rng.integers(0, 1 << 16, n).astype(np.uint16)
-    dport = rng.integers(0, 1 << 16, n).astype(np.uint16)
-    proto = rng.integers(0, 3, n).astype(np.uint8)
+    rules = e.GetACLByName(e.ACLNames()[w.table_id])["rules"] if w.table_id >= 0 else None
+    src, dst, sport, dport, proto = gen.gen_tuples(n, index_base=base, rules=rules, **w.gen)
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
     for _ in range(a.warmup + a.steps):
-        _, cnt = e.debug_classify_host(w.mode, w.table_id, src, dst, sport, dport, proto, counters=True)
+        out, cnt = e.debug_classify_host(w.mode, w.table_id, src, dst, sport, dport, proto, counters=True)
     if world > 1:
         dist.barrier()
     wall = VD.max_over_ranks(time.perf_counter() - t0, "cpu")
-    counters = torch.from_numpy(cnt.astype(np.int64))
+    local = cnt.astype(np.int64)
+    # per-rank self-check: verdicts and hit counters of the whole (small) shard vs the oracle
+    act, slot, hist = OW.expected(e, w.mode, w.table_id, w.local_ifs, w.node_if, src, dst, sport, dport, proto,
+                                  threads=2)
+    par = {"index_base": int(base), "tuples": int(n),
+           "bit_exact_action_and_rule_index": bool(np.array_equal(out >> 30, act.astype(np.uint32)) and
+                                                   np.array_equal(out & 0x3FFFFFFF, slot)),
+           "counters_equal_oracle_histogram": bool(np.array_equal(local, hist)), "evaluations": int(hist.sum())}
+    pars = VD.gather_objects(par)
+    counters = torch.from_numpy(local.copy())
     t1 = time.perf_counter()
     VD.allreduce_counters(counters)
+    ms = (time.perf_counter() - t1) * 1e3
+    # the all-reduced counters == the oracle's histogram over the whole job's index range
     total = VD.sum_over_ranks(n, "cpu")
+    ora = torch.from_numpy(hist.copy())
+    VD.allreduce_counters(ora)
+    check = bool(torch.equal(counters, ora)) and (int(counters.sum()) == total if w.mode != 2
+                                                  else int(counters.sum()) >= total)
     line = {"metric": METRIC, "value": round(total * a.steps / wall / 1e6, 3), "unit": "Mpps", "n_gpus": world,
             "steps": a.steps, "warmup": a.warmup, "scaling": a.scaling, "dry_run": True,
             "config": {"workload": "config%d: %s" % (a.config, w.desc), "tuples_per_gpu": n, "tuples_total": total,
                        "parallelism": "dp%d" % world},
-            "counter_allreduce_ms": round((time.perf_counter() - t1) * 1e3, 3),
-            "counter_allreduce_check": bool(int(counters.sum()) == total if w.mode != 2 else
-                                            int(counters.sum()) >= total),
+            "counter_allreduce_ms": round(ms, 3), "counter_allreduce_check": check,
+            "parity_sample": {"ranks": world, "tuples": sum(p["tuples"] for p in pars),
+                              "bit_exact_action_and_rule_index": all(p["bit_exact_action_and_rule_index"]
+                                                                     for p in pars),
+                              "counters_equal_oracle_histogram": all(p["counters_equal_oracle_histogram"]
+                                                                     for p in pars)},
+            "parity_per_rank": pars,
             "counters_sha": __import__("hashlib").sha1(counters.numpy().tobytes()).hexdigest()[:16]}
     if rank == 0:
         print(json.dumps(line), flush=True)
@@ -350,47 +419,79 @@ def pmc_traffic(config, n, other_shape):
     return int(p["hbm_traffic_bytes_per_launch"] * n / p["tuples_per_launch"]), os.path.basename(files[-1])
 
 
-def cpu_baseline(w, b, out, k, faithful_s=8.0, budget_s=10.0):
-    """The oracle's evalACL/testConnection (oracle/oracle.c) timed on this host's cores over
-    the first k tuples of the same workload (k capped so the run takes about budget_s: a
-    calibration run on 4096 tuples sizes it); also checks the GPU verdicts on that sample."""
+def host_cores():
+    """CPUs this process may use: its affinity set, capped by a cgroup-v2 CPU quota when one is
+    set (a GPU box's share of a larger host)"""
+    n = len(os.sched_getaffinity(0))
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, p = f.read().split()[:2]
+        if q != "max":
+            n = min(n, max(1, int(q) // int(p)))
+    except (OSError, ValueError):
+        pass
+    return max(1, n)
+
+
+def _timed_rate(fn, k_max, budget_s, cal):
+    """fn(k) run on a calibration sample of `cal` tuples, then on a sample sized to about
+    budget_s seconds (at most k_max) -> (tuples/s, sample size, result of the timed call)"""
+    t0 = time.perf_counter()
+    fn(min(cal, k_max))
+    rate = min(cal, k_max) / max(time.perf_counter() - t0, 1e-9)
+    k = int(min(k_max, max(min(cal, k_max), rate * budget_s)))
+    t0 = time.perf_counter()
+    r = fn(k)
+    return k / (time.perf_counter() - t0), k, r
+
+
+def cpu_baseline(w, b, out, k_max, faithful_s=8.0, budget_s=10.0):
+    """The oracle's evalACL / testConnection (oracle/oracle.c, rules pre-parsed: BASELINE.md's
+    B2) timed on this host's cores -- at one thread and at every core the process may use --
+    over the first tuples of the same workload, each sample sized by a calibration run to
+    about budget_s (one thread: half of it); in SINGLE mode also the reference-faithful variant
+    (CIDR strings parsed on every rule visit, as evalACL does; one thread). The verdicts of
+    the multi-thread sample are compared with the GPU's."""
     from oracle import fast, world  # cpu_baseline leg: the checker, never the thing measured on GPU
 
     e = w.engine
-    threads = min(16, os.cpu_count() or 1)
-    k = min(k, b.n)
-    if w.mode == 0:
-        ora = fast.OraACL(e.GetACLByName(e.ACLNames()[w.table_id])["rules"])
-        c = min(4096 * threads, k)
-        cs = b.numpy(c)
-        t0 = time.perf_counter()
-        fast.eval_acl(ora, cs[0], cs[1], cs[3], cs[4], threads=threads)
-        k = int(min(k, max(c, c / max(time.perf_counter() - t0, 1e-9) * budget_s)))
-    src, dst, sport, dport, proto = b.numpy(k)
-    got = out[:k].cpu().numpy().view(np.uint32)
+    cores = host_cores()
+    k_max = min(k_max, b.n)
+    src, dst, sport, dport, proto = b.numpy(k_max)
     extra = {}
-    faithful_ok = None
     if w.mode == 0:
-        t0 = time.perf_counter()
-        act, idx = fast.eval_acl(ora, src, dst, dport, proto, threads=threads)
-        dt = time.perf_counter() - t0
-        base = e.slot_of_rule(w.table_id, 0)
-        dflt = e.slot_of_rule(w.table_id, -1)
-        slot = np.where(idx >= 0, base + idx.astype(np.int64), dflt).astype(np.uint32)
-        kind = "evalACL over the same ACL (rules pre-parsed), %d threads" % threads
-        # reference-faithful variant (CIDR strings parsed per rule visit, one thread): a
-        # 4096-tuple calibration run sizes the sample to about faithful_s seconds
+        wd = world.World(e, {}, None)
+        t = wd.tids.index(w.table_id)
+        ora = wd.acls[t]
+        run = lambda k, th: fast.eval_acl(ora, src[:k], dst[:k], dport[:k], proto[:k], threads=th)
+        to_slot = lambda r: wd.slots(np.full(len(r[1]), t, np.int64), r[1])
+        kind = "evalACL over the same ACL (rules pre-parsed)"
+    else:
+        wd = world.World(e, w.local_ifs, w.node_if)
+        sif, dif = wd.resolve(src), wd.resolve(dst)  # interface lookup kept outside the timed call
+        if w.mode == 1:
+            run = lambda k, th: fast.perpod(wd.acls, wd.if_out, dif[:k], src[:k], dst[:k], dport[:k], proto[:k], th)
+            kind = "evalACL(outbound ACL of the dst interface), rules pre-parsed, interfaces resolved beforehand"
+        else:
+            run = lambda k, th: fast.test_connection(wd.acls, wd.if_in, wd.if_out, sif[:k], dif[:k], src[:k], dst[:k],
+                                                     sport[:k], dport[:k], proto[:k], th)
+            kind = "testConnection (up to 4 evalACL), rules pre-parsed, interfaces resolved beforehand"
+        to_slot = lambda r: wd.slots(r[1], r[2])
+    rate_n, k_n, res = _timed_rate(lambda k: run(k, cores), k_max, budget_s, 4096 * cores)
+    rate_1, k_1, _ = _timed_rate(lambda k: run(k, 1), k_max, budget_s / 2, 4096)
+    got = out[:k_n].cpu().numpy().view(np.uint32)
+    ok = bool(((got >> 30) == res[0].astype(np.uint32)).all() and ((got & 0x3FFFFFFF) == to_slot(res)).all())
+    if w.mode == 0:
         rules = e.GetACLByName(e.ACLNames()[w.table_id])["rules"]
-        cal = 64 if len(rules) > 20000 else 4096
-        t0 = time.perf_counter()
-        fast.eval_acl_faithful(rules, src[:cal], dst[:cal], dport[:cal], proto[:cal])
-        rate = cal / max(time.perf_counter() - t0, 1e-9)
-        kf = int(min(k, max(cal, rate * faithful_s)))
-        t0 = time.perf_counter()
-        fa, fi = fast.eval_acl_faithful(rules, src[:kf], dst[:kf], dport[:kf], proto[:kf])
-        extra["faithful_1thread_mpps"] = round(kf / (time.perf_counter() - t0) / 1e6, 4)
+        fr, kf, (fa, fi) = _timed_rate(lambda k: fast.eval_acl_faithful(rules, src[:k], dst[:k], dport[:k], proto[:k]),
+                                       k_max, faithful_s, 64 if len(rules) > 20000 else 4096)
+        extra["faithful_1thread_mpps"] = round(fr / 1e6, 4)
         extra["faithful_sample"] = kf
-        fslot = np.where(fi >= 0, base + fi.astype(np.int64), dflt).astype(np.uint32)
+        fslot = wd.slots(np.full(len(fi), t, np.int64), fi)
+        extra["faithful_variant_bit_exact"] = bool(((got[:kf] >> 30) == fa.astype(np.uint32)).all() and
+                                                   ((got[:kf] & 0x3FFFFFFF) == fslot[:kf]).all()) \
+            if kf <= k_n else None
+        idx = res[1]
         # rules the reference's first-match loop (aclengine_mock.go:510-649) visits per tuple
         nr = len(rules)
         visited = np.where(idx >= 0, idx.astype(np.int64) + 1, nr)
@@ -398,35 +499,18 @@ def cpu_baseline(w, b, out, k, faithful_s=8.0, budget_s=10.0):
                                             "p99": int(np.percentile(visited, 99)), "rules": nr}
         # ... and the loads the GPU walk makes of the compiled structure per tuple (the kernels'
         # walk code on the host with counting loaders), LDS-staged vs gathered from HBM / L2
-        ks = min(k, 1 << 20)
+        ks = min(k_n, 1 << 20)
         nl, nm, stage = e.debug_walk_stats(w.table_id, src[:ks], dst[:ks], dport[:ks], proto[:ks])
         extra["gpu_loads_per_tuple"] = {"lds_mean": round(float(nl.mean()), 3),
                                         "gather_mean": round(float(nm.mean()), 3),
                                         "gather_p99": int(np.percentile(nm, 99)), "gather_max": int(nm.max()),
                                         "stage": stage, "sample": ks}
-        faithful_ok = bool(((got[:kf] >> 30) == fa.astype(np.uint32)).all() and ((got[:kf] & 0x3FFFFFFF) == fslot).all())
-    else:
-        wd = world.World(e, w.local_ifs, w.node_if)
-        sif, dif = wd.resolve(src), wd.resolve(dst)  # interface lookup kept outside the timed call
-        t0 = time.perf_counter()
-        if w.mode == 1:
-            act, lt, li = fast.perpod(wd.acls, wd.if_out, dif, src, dst, dport, proto, threads)
-            kind = "evalACL(outbound ACL of the dst interface), rules pre-parsed, %d threads" % threads
-        else:
-            act, lt, li = fast.test_connection(wd.acls, wd.if_in, wd.if_out, sif, dif, src, dst, sport, dport, proto,
-                                               threads)
-            kind = "testConnection (up to 4 evalACL), rules pre-parsed, %d threads" % threads
-        dt = time.perf_counter() - t0
-        slot = wd.slots(lt, li)
-        kind += ", interfaces resolved beforehand"
-    ok = bool(((got >> 30) == act.astype(np.uint32)).all() and ((got & 0x3FFFFFFF) == slot).all())
-    base = {"value": round(k / dt / 1e6, 3), "unit": "Mpps", "cores": threads, "host_cpus": os.cpu_count(),
-            "kind": "port", "sample": "first %d tuples of the same workload; %s" % (k, kind)}
+    base = {"value": round(rate_n / 1e6, 3), "unit": "Mpps", "cores": cores, "host_cpus": os.cpu_count(),
+            "kind": "port", "sample": "first %d tuples of the same workload; %s, %d threads" % (k_n, kind, cores),
+            "single_thread": {"value": round(rate_1 / 1e6, 3), "unit": "Mpps", "cores": 1, "sample": k_1},
+            "sample_bit_exact_vs_gpu": ok}
     base.update(extra)
-    parity = {"tuples": k, "bit_exact_action_and_rule_index": ok}
-    if faithful_ok is not None:
-        parity["faithful_variant_bit_exact"] = faithful_ok
-    return base, parity
+    return base
 
 
 if __name__ == "__main__":

@@ -288,7 +288,10 @@ int pg_counters_snapshot(const pg_ctx* ctx, uint64_t* host_out, size_t n);
  * One process driving several GPUs: pg_comm_init_all over one context per GPU.
  * pg_allreduce_counters / pg_allreduce_counters_all first check that every rank compiled the
  * same counter layout (slots, ACL names, rules per ACL; PG_EFAULT if not, nothing reduced), then
- * sum the device counters in place (ncclAllReduce u64 sum) and refresh the host snapshots.
+ * sum a device copy of the counters (ncclAllReduce u64 sum) into the host snapshots. The
+ * device counters keep this rank's own counts (pg_read_counters still returns them), so a
+ * periodic gauge may all-reduce again without a reset in between. The caller's current device
+ * is restored on every return path.
  * Synchronous. RCCL (librccl.so.1) is loaded on first use. */
 #define PG_COMM_ID_BYTES 128
 int pg_comm_unique_id(uint8_t id[PG_COMM_ID_BYTES]);

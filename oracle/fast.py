@@ -29,7 +29,7 @@ def _load():
     lib.ora_acl_new.argtypes = [C.POINTER(ora_rule), C.c_int]
     lib.ora_acl_free.argtypes = [P]
     lib.ora_eval.argtypes = [P, P, P, P, P, C.c_size_t, P, P, C.c_int]
-    lib.ora_conn.argtypes = [P, P, P, P, P, P, P, P, P, P, C.c_size_t, P, P, P, C.c_int]
+    lib.ora_conn.argtypes = [P, P, P, P, P, P, P, P, P, P, C.c_size_t, P, P, P, P, P, C.c_int]
     lib.ora_perpod.argtypes = [P, P, P, P, P, P, P, C.c_size_t, P, P, P, C.c_int]
     return lib
 
@@ -104,9 +104,13 @@ def eval_acl_faithful(rules_dicts, src, dst, dport, proto):
     return act, idx
 
 
-def test_connection(acls, if_in, if_out, sif, dif, src, dst, sport, dport, proto, threads=os.cpu_count() or 1):
+def test_connection(acls, if_in, if_out, sif, dif, src, dst, sport, dport, proto, threads=os.cpu_count() or 1,
+                    trace=False):
     """testConnection per tuple over resolved interfaces. acls: list of OraACL (table id order).
-    Returns (ConnAction, last evaluated table (-1 none/-2 unresolved), last matched index)."""
+    Returns (ConnAction, last evaluated table (-1 none/-2 unresolved), last matched index);
+    trace=True also returns every evaluation the connection made, in the order
+    aclengine_mock.go:448-491 makes them: (tables int32[n, 4], indices int32[n, 4]), table -3 =
+    no evaluation, -2 = the unresolved-interface FAILURE, -1 = no ACL (nil: PERMIT)."""
     n = len(src)
     harr = (C.c_void_p * max(1, len(acls)))(*[a.h for a in acls])
     cv = lambda a, dt: np.ascontiguousarray(a, dt)
@@ -114,8 +118,14 @@ def test_connection(acls, if_in, if_out, sif, dif, src, dst, sport, dport, proto
     src, dst, sport, dport, proto = (cv(src, np.uint32), cv(dst, np.uint32), cv(sport, np.uint16),
                                      cv(dport, np.uint16), cv(proto, np.uint8))
     conn, lt, li = np.empty(n, np.int32), np.empty(n, np.int32), np.empty(n, np.int32)
+    evt = evi = None
+    if trace:
+        evt, evi = np.empty((n, 4), np.int32), np.empty((n, 4), np.int32)
     lib.ora_conn(C.cast(harr, C.c_void_p), _p(if_in), _p(if_out), _p(sif), _p(dif), _p(src), _p(dst), _p(sport),
-                 _p(dport), _p(proto), n, _p(conn), _p(lt), _p(li), threads)
+                 _p(dport), _p(proto), n, _p(conn), _p(lt), _p(li), _p(evt) if trace else None,
+                 _p(evi) if trace else None, threads)
+    if trace:
+        return conn, lt, li, evt, evi
     return conn, lt, li
 
 

@@ -6,7 +6,8 @@
  *   evalACL          :503-652   (ora_eval_faithful: parses the CIDR strings on every rule
  *                                visit exactly like the Go loop; ora_eval: same loop over
  *                                rules parsed once per ACL, multi-threaded)
- *   testConnection   :424-501   (ora_conn)
+ *   testConnection   :424-501   (ora_conn; optionally every evaluation it makes, in order:
+ *                                the hit-counter histogram of a connection batch)
  * and Go 1.11 net.ParseCIDR / IPNet.Contains for IPv4 packets (src/net/ip.go), which the
  * evalACL loop calls per rule visit.  Independent of the product code in vpp_amd/csrc.
  * Pinned through oracle/aclengine.py (itself pinned by the reference's KATs) by
@@ -330,13 +331,26 @@ typedef struct {
     const uint16_t *sport, *dport;
     const uint8_t* proto;
     int32_t *conn, *last_table, *last_idx;
+    int32_t *ev_table, *ev_idx; /* optional: every evaluation, 4 per tuple (-3 = none) */
     size_t lo, hi;
 } conn_job;
 
+/* Every evalACL a connection makes is recorded in order (ev_table/ev_idx, up to 4 per
+ * tuple, -3 = not made) when the caller asks for it: the per-rule hit counters of
+ * testConnection count exactly these (the unresolved-interface FAILURE counts once, as
+ * table -2). */
 static int conn_one(const conn_job* j, size_t i, int32_t* lt, int32_t* li) {
     int32_t si = j->sif[i], di = j->dif[i];
+    int32_t* evt = j->ev_table ? j->ev_table + 4 * i : NULL;
+    int32_t* evi = j->ev_idx ? j->ev_idx + 4 * i : NULL;
+    int nev = 0;
+    if (evt)
+        for (int k = 0; k < 4; k++) evt[k] = -3, evi[k] = -1;
     *lt = -2; *li = -1;
-    if (si < 0 || di < 0) return 3;
+    if (si < 0 || di < 0) {
+        if (evt) evt[0] = -2;
+        return 3;
+    }
     int same = si == di;
     int srefl = 0, drefl = 0, a;
     int pr = j->proto[i];
@@ -346,6 +360,8 @@ static int conn_one(const conn_job* j, size_t i, int32_t* lt, int32_t* li) {
         int32_t t_ = (tab);                                                      \
         *lt = t_;                                                                \
         a = eval_one(t_ >= 0 ? j->acls[t_] : NULL, x, y, pr, port, li);          \
+        if (evt) evt[nev] = t_, evi[nev] = *li;                                  \
+        nev++;                                                                   \
     } while (0)
     EV(j->if_in[si], s, d, j->dport[i]);
     if (a == A_FAILURE) return 3;
@@ -380,7 +396,7 @@ static void* conn_worker(void* p) {
 int ora_conn(const ora_acl* const* acls, const int32_t* if_in, const int32_t* if_out, const int32_t* sif,
              const int32_t* dif, const uint32_t* src, const uint32_t* dst, const uint16_t* sport, const uint16_t* dport,
              const uint8_t* proto, size_t n, int32_t* out_conn, int32_t* out_last_table, int32_t* out_last_idx,
-             int threads) {
+             int32_t* ev_table, int32_t* ev_idx, int threads) {
     if (threads < 1) threads = 1;
     if (threads > 256) threads = 256;
     pthread_t th[256];
@@ -390,7 +406,7 @@ int ora_conn(const ora_acl* const* acls, const int32_t* if_in, const int32_t* if
         size_t lo = t * per, hi = (t + 1) * per < n ? (t + 1) * per : n;
         if (lo > hi) lo = hi;
         jobs[t] = (conn_job){acls, if_in, if_out, sif, dif, src, dst, sport, dport, proto, out_conn, out_last_table,
-                             out_last_idx, lo, hi};
+                             out_last_idx, ev_table, ev_idx, lo, hi};
         pthread_create(&th[t], NULL, conn_worker, &jobs[t]);
     }
     for (int t = 0; t < threads; t++) pthread_join(th[t], NULL);
@@ -426,7 +442,7 @@ int ora_perpod(const ora_acl* const* acls, const int32_t* if_out, const int32_t*
         size_t lo = t * per, hi = (t + 1) * per < n ? (t + 1) * per : n;
         if (lo > hi) lo = hi;
         jobs[t] = (conn_job){acls, NULL, if_out, NULL, dif, src, dst, NULL, dport, proto, out_action, out_table,
-                             out_idx, lo, hi};
+                             out_idx, NULL, NULL, lo, hi};
         pthread_create(&th[t], NULL, perpod_worker, &jobs[t]);
     }
     for (int t = 0; t < threads; t++) pthread_join(th[t], NULL);

@@ -30,7 +30,8 @@ class World:
         self.local_if = np.array([self.ifx[local_ifs[ip]] if ip in local_ifs else -1 for ip in ips], np.int32)
         self.node = self.ifx[node_if] if node_if else -1
         # slot layout of the engine (pg_table_info / pg_num_counter_slots)
-        info = [engine.table_info(engine.table_id(n)) for n in self.names]
+        self.tids = [engine.table_id(n) for n in self.names]  # engine table id of each oracle table
+        info = [engine.table_info(t) for t in self.tids]
         self.base = np.array([b for b, _, _ in info] + [0], np.int64)
         self.dflt = np.array([d for _, _, d in info] + [0], np.int64)
         ns = engine.num_counter_slots()
@@ -58,8 +59,40 @@ class World:
         act, lt, li = fast.perpod(self.acls, self.if_out, self.resolve(dst), src, dst, dport, proto, threads)
         return act, self.slots(lt, li)
 
-    def conn(self, src, dst, sport, dport, proto, threads=1):
-        """-> (ConnAction, slot of the deciding evaluation) of testConnection."""
-        c, lt, li = fast.test_connection(self.acls, self.if_in, self.if_out, self.resolve(src), self.resolve(dst),
-                                         src, dst, sport, dport, proto, threads)
-        return c, self.slots(lt, li)
+    def single(self, table_id, src, dst, dport, proto, threads=1):
+        """-> (ACLAction, slot) of evalACL over the engine's table `table_id`."""
+        t = self.tids.index(table_id)
+        act, idx = fast.eval_acl(self.acls[t], src, dst, dport, proto, threads=threads)
+        return act, self.slots(np.full(len(idx), t, np.int64), idx)
+
+    def conn(self, src, dst, sport, dport, proto, threads=1, hist=False):
+        """-> (ConnAction, slot of the deciding evaluation) of testConnection; hist=True also
+        the per-rule hit-counter histogram of the batch: one count per evalACL every
+        connection makes (up to four, aclengine_mock.go:448-491), at the slot of the rule that
+        decided that evaluation (its table's default slot when none matched, "no ACL" for a
+        nil ACL), and one "unresolved" count per connection with an unknown interface."""
+        r = fast.test_connection(self.acls, self.if_in, self.if_out, self.resolve(src), self.resolve(dst),
+                                 src, dst, sport, dport, proto, threads, trace=hist)
+        if not hist:
+            c, lt, li = r
+            return c, self.slots(lt, li)
+        c, lt, li, evt, evi = r
+        made = evt.ravel() != -3
+        ev_slots = self.slots(evt.ravel()[made], evi.ravel()[made])
+        h = np.bincount(ev_slots, minlength=self.slot_unresolved + 1).astype(np.int64)
+        return c, self.slots(lt, li), h
+
+
+def expected(engine, mode, table_id, local_ifs, node_if, src, dst, sport, dport, proto, threads=1):
+    """The oracle's answer for a batch in any mode (0 SINGLE: evalACL over table_id; 1 PERPOD:
+    evalACL over the outbound ACL of dst's interface; 2 CONN: testConnection) -> (action,
+    deciding slot, per-rule hit-counter histogram). SINGLE and PERPOD make one evaluation per
+    tuple, so their histogram is that of the slots; CONN counts every evaluation it makes."""
+    wd = World(engine, local_ifs, node_if)
+    if mode == 0:
+        act, slot = wd.single(table_id, src, dst, dport, proto, threads)
+    elif mode == 1:
+        act, slot = wd.perpod(src, dst, dport, proto, threads)
+    else:
+        return wd.conn(src, dst, sport, dport, proto, threads, hist=True)
+    return act, slot, np.bincount(slot, minlength=wd.slot_unresolved + 1).astype(np.int64)

@@ -277,6 +277,10 @@ def test_rccl_counter_allreduce_single_rank():
     summed = D.allreduce_counters(e)
     assert np.array_equal(summed, hist) and np.array_equal(D.read_counters(e), hist)
     assert np.array_equal(D.counters_snapshot(e), hist)
+    # a second reduction (a periodic gauge) sums the same local counts again: no compounding,
+    # and the local counters are still this rank's own
+    assert np.array_equal(D.allreduce_counters(e), hist) and np.array_equal(D.read_counters(e), hist)
+    assert torch.cuda.current_device() == 0
     e2, _ = _small_engine(10)
     D.comm_init_all([e2])
     D.reset_counters(e2)

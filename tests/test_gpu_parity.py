@@ -216,16 +216,22 @@ def test_conn_and_perpod_modes_random_topology(seed):
     b = D.TupleBatch.from_numpy(*tup)
     sm = slot_map(e)
 
-    # CONN
+    # CONN, with hit counters: one count per evalACL each connection makes
     out = torch.empty(n, dtype=torch.int32, device="cuda")
-    D.classify(e, MODE_CONN, -1, b, out)
+    cnt = torch.zeros(e.num_counter_slots(), dtype=torch.int64, device="cuda")
+    D.classify(e, MODE_CONN, -1, b, out, counters=cnt)
     torch.cuda.synchronize()
     got = out.cpu().numpy().view(np.uint32)
-    conn, lt, li = fast.test_connection(ora, if_in, if_out, sif, dif, src, dst, sport, dport, proto)
-    exp_slot = np.array([sm[(int(t), int(i))] if t >= 0 and i >= 0 else (sm[(int(t), -1)] if t >= 0 else sm[(-1, -1)])
-                         for t, i in zip(lt, li)], np.uint32)
+    conn, lt, li, evt, evi = fast.test_connection(ora, if_in, if_out, sif, dif, src, dst, sport, dport, proto,
+                                                  trace=True)
+    to_slot = lambda t, i: sm[(int(t), int(i))] if t >= 0 and i >= 0 else (sm[(int(t), -1)] if t >= 0 else sm[(-1, -1)])
+    exp_slot = np.array([to_slot(t, i) for t, i in zip(lt, li)], np.uint32)
     assert ((got >> 30) == conn.astype(np.uint32)).all(), np.nonzero((got >> 30) != conn)[0][:10]
     assert ((got & 0x3FFFFFFF) == exp_slot).all()
+    made = evt != -3
+    assert (evt != -2).all()  # every end point resolves in this topology
+    hist = np.bincount([to_slot(t, i) for t, i in zip(evt[made], evi[made])], minlength=cnt.numel())
+    assert np.array_equal(cnt.cpu().numpy(), hist)
 
     # PERPOD: evalACL(outbound ACL of dst's interface)
     D.classify(e, MODE_PERPOD, -1, b, out)
@@ -279,8 +285,12 @@ def test_cluster_configs_gpu_vs_oracle(config):
         # one evaluation per tuple: the counters are the histogram of the verdict slots
         assert np.array_equal(cnt.cpu().numpy(), np.bincount(got & 0x3FFFFFFF, minlength=cnt.numel()))
     else:
-        act, slot = wd.conn(src, dst, sport, dport, proto, threads=16)
-        assert int(cnt.sum()) >= b.n  # every connection evaluates at least one ACL
+        # the per-rule hit counters (the statscollector stream) equal the oracle's histogram of
+        # every evalACL the connections made (aclengine_mock.go:448-491, up to four each)
+        act, slot, hist = wd.conn(src, dst, sport, dport, proto, threads=16, hist=True)
+        c = cnt.cpu().numpy()
+        assert np.array_equal(c, hist), np.nonzero(c != hist)[0][:10]
+        assert int(c.sum()) > b.n  # some connections evaluate more than one ACL
     assert ((got >> 30) == act.astype(np.uint32)).all()
     assert ((got & 0x3FFFFFFF) == slot).all()
     assert len(np.unique(got >> 30)) >= 2
@@ -310,7 +320,8 @@ def test_k8s_object_cluster_gpu_vs_oracle(mode):
         act, slot = wd.perpod(src, dst, dport, proto, threads=16)
         assert np.array_equal(cnt.cpu().numpy(), np.bincount(got & 0x3FFFFFFF, minlength=cnt.numel()))
     else:
-        act, slot = wd.conn(src, dst, sport, dport, proto, threads=16)
+        act, slot, hist = wd.conn(src, dst, sport, dport, proto, threads=16, hist=True)
+        assert np.array_equal(cnt.cpu().numpy(), hist)
     assert ((got >> 30) == act.astype(np.uint32)).all()
     assert ((got & 0x3FFFFFFF) == slot).all()
     assert len(np.unique(got >> 30)) >= 2

@@ -99,9 +99,10 @@ def test_two_rank_product_shards_and_counter_allreduce(config):
     src, dst, sport, dport, proto = _gen(w, 0, world * N_PER_RANK)
     if w.mode == 2:  # config 1: testConnection (CONN)
         wd = World(w.engine, w.local_ifs, w.node_if)
-        act, slot = wd.conn(src, dst, sport, dport, proto, threads=2)
-        # CONN counts every evaluation of testConnection: at least one per tuple
-        assert sum(reduced) >= world * N_PER_RANK
+        # CONN counts every evalACL testConnection makes: the oracle's per-evaluation histogram
+        act, slot, hist = wd.conn(src, dst, sport, dport, proto, threads=2, hist=True)
+        assert reduced == hist.tolist()
+        assert sum(reduced) > world * N_PER_RANK
     else:  # config 2: evalACL of the single table, one evaluation per tuple
         from oracle import fast
         e = w.engine
@@ -146,12 +147,26 @@ def test_bench_launcher_two_ranks_cpu_dry_run(scaling):
     d = _bench(*args)
     assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "dp2" and d["scaling"] == scaling
     assert d["counter_allreduce_check"] is True
+    # every rank checked its own shard against the oracle: verdicts and hit counters
+    assert [p["index_base"] for p in d["parity_per_rank"]] == [0, d["parity_per_rank"][0]["tuples"]]
+    assert all(p["bit_exact_action_and_rule_index"] and p["counters_equal_oracle_histogram"]
+               for p in d["parity_per_rank"])
+    assert d["parity_sample"]["tuples"] == d["config"]["tuples_total"]
     if scaling == "strong":
         assert d["config"]["tuples_total"] == 20001
     else:
         assert d["config"]["tuples_total"] == 2 * d["config"]["tuples_per_gpu"]
     one = _bench("--gpus", "1", "--cpu-dry-run", "--config", "2", "--steps", "1", "--warmup", "0")
-    assert one["n_gpus"] == 1
+    assert one["n_gpus"] == 1 and one["parity_sample"]["bit_exact_action_and_rule_index"]
+
+
+def test_bench_two_ranks_conn_counters_cpu_dry_run():
+    """config 5 (testConnection with hit counters) over two ranks: each rank's counters equal
+    the oracle's per-evaluation histogram of its shard, and the summed counters that of the
+    whole job."""
+    d = _bench("--gpus", "2", "--cpu-dry-run", "--config", "5", "--tuples", "6000", "--steps", "1", "--warmup", "0")
+    assert d["counter_allreduce_check"] is True and d["parity_sample"]["counters_equal_oracle_histogram"]
+    assert all(p["evaluations"] > p["tuples"] for p in d["parity_per_rank"])
 
 
 def test_bench_rejects_world_mismatch():

@@ -798,7 +798,9 @@ int pg_reset_counters(pg_ctx* ctx, void* stream) {
     int rc = ctx->eng.sync();
     if (rc) return rc;
     std::string err;
-    if (dev_memset(ctx->eng.counters, 0, ctx->eng.counter_slots * 8, stream, &err) != 0)
+    // the reset is a counter write on `stream`: pg_read_counters waits for it like for a launch
+    if (dev_memset(ctx->eng.counters, 0, ctx->eng.counter_slots * 8, stream, &err) != 0 ||
+        dev_mark_use(ctx->eng.cur, stream, true, &err) != 0)
         return fail(ctx, PG_EIO, err);
     return PG_OK;
 }
@@ -893,12 +895,28 @@ int pg_comm_rank(const pg_ctx* ctx, int* rank, int* nranks) {
     return ctx->eng.comm ? PG_OK : PG_ENOENT;
 }
 
-// The contexts' counters summed in place over their communicator (k = 1: this process's rank
-// of a multi-process communicator; k > 1: every context of one pg_comm_init_all group, in one
-// RCCL group call). First a max all-reduce of {slots, layout hash, ~slots, ~hash} proves that
-// every rank compiled the same counter layout (a mismatched all-reduce would hang or mix
-// slots); then ncclAllReduce(u64, sum). Synchronous; the host snapshots are refreshed.
+// Restores the device that was current when it was made, whatever the calls in between set
+// (the all-reduce below visits every context's GPU).
+struct RestoreDevice {
+    int prev = -1;
+    RestoreDevice() {
+        if (dev_get_device(&prev) != 0) prev = -1;
+    }
+    ~RestoreDevice() {
+        int now = -1;
+        if (prev >= 0 && (dev_get_device(&now) != 0 || now != prev)) (void)dev_set_device(prev, nullptr);
+    }
+};
+
+// The contexts' counters summed over their communicator (k = 1: this process's rank of a
+// multi-process communicator; k > 1: every context of one pg_comm_init_all group, in one RCCL
+// group call). First a max all-reduce of {slots, layout hash, ~slots, ~hash} proves that every
+// rank compiled the same counter layout (a mismatched all-reduce would hang or mix slots);
+// then ncclAllReduce(u64, sum) of a device copy of the counters: the counters themselves stay
+// this rank's own, so a periodic gauge may reduce again without compounding earlier sums.
+// Synchronous; the host snapshots hold the sums afterwards.
 static int allreduce_counters(pg_ctx* const* ctxs, int k, void* const* streams) {
+    RestoreDevice restore;
     std::vector<void*> comms(k), sts(k);
     std::vector<unsigned long long*> chk(k), bufs(k);
     std::vector<int> devs(k);
@@ -909,18 +927,25 @@ static int allreduce_counters(pg_ctx* const* ctxs, int k, void* const* streams) 
         Engine& E = c->eng;
         if (!E.comm) return fail(c, PG_EINVAL, "no communicator (pg_comm_init_rank / pg_comm_init_all)");
         if (k > 1 && E.comm_nranks != k) return fail(c, PG_EINVAL, "contexts are not one pg_comm_init_all group");
-        DeviceGuard g(c);
-        if (!g.ok) return fail(c, PG_EIO, g.err);
+        if (dev_set_device(E.device, &err) != 0) return fail(c, PG_EIO, err);
         int rc = E.sync();
         if (rc) return rc;
+        if (E.reduced_slots != E.counter_slots) {
+            if (E.reduced) dev_release(E.reduced);
+            E.reduced_slots = 0;
+            if (!(E.reduced = (unsigned long long*)dev_alloc(E.counter_slots * 8, &err)))
+                return fail(c, PG_ENOMEM, err);
+            E.reduced_slots = E.counter_slots;
+        }
         const uint64_t n = E.counter_slots, h = E.layout_hash;
         const uint64_t v[4] = {n, h, ~n, ~h};
-        if (dev_wait_uses(E.cur, &err) != 0 || dev_copy_h2d(E.comm_check, v, sizeof v, &err) != 0)
+        sts[i] = streams ? streams[i] : nullptr;
+        if (dev_wait_uses(E.cur, &err) != 0 || dev_copy_h2d(E.comm_check, v, sizeof v, &err) != 0 ||
+            dev_copy_d2d_async(E.reduced, E.counters, E.counter_slots * 8, sts[i], &err) != 0)
             return fail(c, PG_EIO, err);
-        comms[i] = E.comm, sts[i] = streams ? streams[i] : nullptr, chk[i] = E.comm_check;
-        bufs[i] = E.counters, devs[i] = E.device;
+        comms[i] = E.comm, chk[i] = E.comm_check;
+        bufs[i] = E.reduced, devs[i] = E.device;
     }
-    DeviceGuard g(ctxs[0]);
     if (dev_comm_allreduce_u64(comms.data(), chk.data(), devs.data(), sts.data(), k, 4, true, &err) != 0)
         return fail(ctxs[0], PG_EIO, err);
     for (int i = 0; i < k; i++) {
@@ -940,7 +965,7 @@ static int allreduce_counters(pg_ctx* const* ctxs, int k, void* const* streams) 
         Engine& E = ctxs[i]->eng;
         E.snapshot.resize(E.counter_slots);
         if (dev_set_device(E.device, &err) != 0 || dev_stream_sync(sts[i], &err) != 0 ||
-            dev_copy_d2h(E.snapshot.data(), E.counters, E.counter_slots * 8, &err) != 0)
+            dev_copy_d2h(E.snapshot.data(), E.reduced, E.counter_slots * 8, &err) != 0)
             return fail(ctxs[i], PG_EIO, err);
     }
     return PG_OK;

@@ -88,6 +88,10 @@ int dev_copy_h2d(void* dst, const void* src, size_t bytes, std::string* err) {
     HIPCHK(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice));
     return 0;
 }
+int dev_copy_d2d_async(void* dst, const void* src, size_t bytes, void* stream, std::string* err) {
+    HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, (hipStream_t)stream));
+    return 0;
+}
 int dev_sync(std::string* err) {
     HIPCHK(hipDeviceSynchronize());
     return 0;
@@ -110,6 +114,17 @@ int dev_mark_use(DeviceBuffers* b, void* stream, bool fenced, std::string* err) 
             (fenced ? u.fenced_rec : u.plain_rec) = true;
             return 0;
         }
+    // bounded list: past kMaxUses streams, wait for the recorded launches and start over
+    constexpr size_t kMaxUses = 32;
+    if (b->uses.size() >= kMaxUses) {
+        for (auto& u : b->uses) {
+            if (u.plain_rec) HIPCHK(hipEventSynchronize(u.plain));
+            if (u.fenced_rec) HIPCHK(hipEventSynchronize(u.fenced));
+            (void)hipEventDestroy(u.plain);
+            (void)hipEventDestroy(u.fenced);
+        }
+        b->uses.clear();
+    }
     DeviceBuffers::Use u{s, nullptr, nullptr, false, false};
     HIPCHK(hipEventCreateWithFlags(&u.plain, hipEventDisableTiming | hipEventDisableSystemFence));
     HIPCHK(hipEventCreateWithFlags(&u.fenced, hipEventDisableTiming));

@@ -228,6 +228,7 @@ void dev_release(void* p);
 int dev_memset(void* p, int v, size_t bytes, void* stream, std::string* err);
 int dev_copy_d2h(void* dst, const void* src, size_t bytes, std::string* err);
 int dev_copy_h2d(void* dst, const void* src, size_t bytes, std::string* err);
+int dev_copy_d2d_async(void* dst, const void* src, size_t bytes, void* stream, std::string* err);
 int dev_sync(std::string* err);
 int dev_stream_sync(void* stream, std::string* err);
 // record that `stream` launched kernels reading table set b (dev_free / dev_wait_uses wait for them)

@@ -146,6 +146,7 @@ DevRule compile_acl_rule(const AclRule& r) {
 Engine::~Engine() {
     if (comm) dev_comm_destroy(comm);
     if (comm_check) dev_release(comm_check);
+    if (reduced) dev_release(reduced);
     if (cur) dev_free(cur);
     if (counters) dev_release(counters);
 }

@@ -52,6 +52,10 @@ struct Engine {
     void* comm = nullptr;
     int comm_rank = -1, comm_nranks = 0;
     unsigned long long* comm_check = nullptr;
+    // the all-reduce sums a copy of the counters (never the counters themselves), so the
+    // local counts stay this rank's and repeated reductions do not compound
+    unsigned long long* reduced = nullptr;
+    size_t reduced_slots = 0;
     // host copy of the counters as last all-reduced / read (pg_counters_snapshot: the
     // statscollector gauge reads it without touching the GPU)
     std::vector<uint64_t> snapshot;

@@ -151,7 +151,8 @@ def comm_init_all(engines):
 
 
 def allreduce_counters(engine, stream=None):
-    """sum this rank's device counters over the communicator (in place) -> the summed counters"""
+    """sum this rank's device counters over the communicator -> the summed counters (the
+    device counters themselves keep this rank's counts)"""
     engine._ck(lib.pg_allreduce_counters(engine.h, _stream_ptr(stream)))
     return counters_snapshot(engine)
 

@@ -62,3 +62,13 @@ def max_over_ranks(value, device):
     t = torch.tensor([value], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+def gather_objects(obj):
+    """Every rank's (picklable) object, in rank order, on every rank (a list of one without a
+    process group): the per-rank self-checks of the bench line."""
+    if not dist.is_initialized():
+        return [obj]
+    out = [None] * dist.get_world_size()
+    dist.all_gather_object(out, obj)
+    return out
