@@ -386,3 +386,32 @@ def test_large_table_root_staged_and_hbm_walks_equal_oracle():
         assert ((got >> 30) == ea).all() and ((got & 0x3FFFFFFF) == es).all()
         outs.append(got)
     assert np.array_equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("mode", [MODE_PERPOD, MODE_CONN])
+def test_large_node_set_counter_windows_vs_oracle(mode):
+    """Config 6 (K8s objects -> 52 tables, 64.6k rules: more counter slots than the full LDS
+    histogram) with hit counters through the node classifier: per-table LDS windows
+    (node_hist_cells cells; a tiny budget; none = global atomics only) all give counters equal to
+    the oracle's histogram (PERPOD: of the verdict slots; CONN: of every evaluation), and the
+    verdicts stay bit-exact."""
+    from oracle import world as OW
+    from vpp_amd import workloads as W
+    w = W.config6(0, n_tuples=1 << 20)
+    e = w.engine
+    assert e.num_counter_slots() > 16382 and e.node_stats() is not None
+    b = D.TupleBatch(w.n_tuples, with_sport=True)
+    D.gen_tuples(e, b, **w.gen)
+    torch.cuda.synchronize()
+    tup = b.numpy(b.n)
+    act, slot, hist = OW.expected(e, mode, -1, w.local_ifs, w.node_if, *tup, threads=16)
+    for cells in (4096, 300, 0):
+        e.set_tuning("node_hist_cells", cells)
+        out = torch.empty(b.n, dtype=torch.int32, device="cuda")
+        cnt = torch.zeros(e.num_counter_slots(), dtype=torch.int64, device="cuda")
+        D.classify(e, mode, -1, b, out, counters=cnt)
+        torch.cuda.synchronize()
+        got = out.cpu().numpy().view(np.uint32)
+        assert ((got >> 30) == act.astype(np.uint32)).all() and ((got & 0x3FFFFFFF) == slot).all(), cells
+        c = cnt.cpu().numpy()
+        assert np.array_equal(c, hist), (cells, np.nonzero(c != hist)[0][:10])

@@ -1,6 +1,8 @@
 #!/bin/bash
-# A/B of two builds (sweep.py in alternating processes) on the given configs, 2 rounds.
-#   gpurun -- bash tools/r02_ab_lib.sh TAG "libA libB" "3 5c 6" [pytest paths]
+# A/B of builds (tools/sweep.py in alternating processes) on the given configs, 2 rounds.
+# Builds: make -C vpp_amd/csrc variant V=name DEFS="-DPG_...=..." -> vpp_amd/libpolicygpu_name.so
+# Configs: 3, 5c (with counters), r10000 (config 2 at 10k rules), ...
+#   gpurun -- bash tools/ab.sh TAG "libA libB" "3 5c 6" [pytest paths]
 set -o pipefail
 TAG=${1:-ablib}; LIBS=${2:-libpolicygpu.so}; CONFIGS=${3:-3}; TESTS=${4:-}
 R=$(pwd)

@@ -26,12 +26,12 @@ cd /tmp && export TMPDIR=/tmp
 for c in $CONFIGS; do
     step rocprof config $c
     timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof_c$c" -o run -- \
-        python3 "$R/bench.py" --config "$c" --no-cpu > "$O/prof_c$c.log" 2>&1 \
+        python3 "$R/bench.py" --config "$c" --no-cpu --no-check > "$O/prof_c$c.log" 2>&1 \
         || { tail -20 "$O/prof_c$c.log"; exit 1; }
     for ctr in FETCH_SIZE WRITE_SIZE; do
         step pmc $ctr config $c
         timeout -s KILL 120 rocprofv3 --pmc $ctr --output-format csv -d "$O/pmc_${ctr}_c$c" -o run -- \
-            python3 "$R/bench.py" --config "$c" --no-cpu --steps 3 --warmup 1 > "$O/pmc_${ctr}_c$c.log" 2>&1 \
+            python3 "$R/bench.py" --config "$c" --no-cpu --no-check --steps 3 --warmup 1 > "$O/pmc_${ctr}_c$c.log" 2>&1 \
             || { tail -20 "$O/pmc_${ctr}_c$c.log"; exit 1; }
     done
 done

@@ -238,7 +238,8 @@ PG_HD void probe_q(const DevTableSet& T, const uint32_t (&ip)[Q], End (&e)[Q]) {
 // slots on the host
 // kFullLds: lds (when set) holds every slot (node kernels); kAggGlobal: with lds unset, global
 // increments are aggregated per distinct slot over the wave (PERPOD node kernels)
-template <bool kFullLds = false, bool kAggGlobal = false>
+// kWin: node kernels, which may count through per-table windows (twin)
+template <bool kFullLds = false, bool kAggGlobal = false, bool kWin = false>
 struct HistT {
     uint32_t* lds;
     unsigned long long* glob;
@@ -251,6 +252,45 @@ struct HistT {
     // lanes of a wave on one LDS address serialise their atomics
     uint32_t hot = 0xFFFFFFFFu;
     mutable uint32_t nhot = 0;
+    // node kernels over a table set with more slots than the full histogram (device.hpp
+    // HistWindows): twin = the per-table windows {rb, n, cb, h} in LDS, wlds = their cells,
+    // nr = the set's rule count (slots from nr up count in cells slot - nr)
+    const uint32_t* twin = nullptr;  // uint4 per table
+    uint32_t* wlds = nullptr;
+    uint32_t nr = 0, hotcell = 0;  // hotcell: the window cell of `hot`
+    // one increment of an evaluation of table t (t < 0: no table; its slot is past the rules)
+    PG_HD void inc_t(uint32_t slot, int32_t t) const {
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(PG_PROBE_NOINC)
+        if (kWin && twin) {
+            if (slot == hot) {
+                nhot++;
+                return;
+            }
+            uint32_t cell = slot - nr;
+            if (slot < nr) {
+                const uint4 w = reinterpret_cast<const uint4*>(twin)[t < 0 ? 0 : t];
+                const uint32_t off = slot - w.x;
+                cell = off < w.w ? w.z + off : (off == w.y - 1u ? w.z + w.w : 0xFFFFFFFFu);
+            }
+            if (cell != 0xFFFFFFFFu) {
+                atomicAdd(&wlds[cell], 1u);
+                return;
+            }
+            // outside every window: one global atomic per distinct slot over the wave's lanes
+            for (;;) {
+                const uint32_t lead = __builtin_amdgcn_readfirstlane(slot);
+                const unsigned long long m = __ballot(slot == lead);
+                if (slot == lead) {
+                    if (__lane_id() == (unsigned)(__ffsll((long long)m) - 1))
+                        atomicAdd(&glob[lead], (unsigned long long)__popcll(m));
+                    break;
+                }
+            }
+            return;
+        }
+#endif
+        inc(slot);
+    }
     PG_HD void inc(uint32_t slot) const {
 #if defined(__HIP_DEVICE_COMPILE__) && defined(PG_PROBE_NOINC)  // measurement build only
         if (slot == 0xFFFFFFFFu) lds[0] = 0;
@@ -324,7 +364,8 @@ struct HistT {
             const uint32_t n = nhot;
             nhot = 0;
             const uint32_t c = h0 - wbase;
-            if (lds && (kFullLds || full)) atomicAdd(&lds[h0], n);
+            if (kWin && twin) atomicAdd(&wlds[hotcell], n);
+            else if (lds && (kFullLds || full)) atomicAdd(&lds[h0], n);
             else if (lds && c < wn) atomicAdd(&lds[c], n);
             else if (lds && h0 == xslot) atomicAdd(&lds[wn], n);
             else if (lds && h0 == xslot1) atomicAdd(&lds[wn + 1], n);
@@ -631,7 +672,7 @@ PG_HD void eval_step(const DevTableSet& T, const EV& ev, const int32_t (&t)[Q], 
     if (COUNT) {
         PG_UNROLL
         for (int j = 0; j < Q; j++)
-            if (run[j]) h.inc(w[j] & kSlotMask);
+            if (run[j]) h.inc_t(w[j] & kSlotMask, t[j]);
     }
 }
 
@@ -651,7 +692,7 @@ PG_HD void conn_q(const DevTableSet& T, const EV& ev, const End (&es)[Q], const 
         w[j] = 0;
         if (!live[j]) {
             out[j] = verdict(3u, T.slot_unresolved);
-            if (COUNT) h.inc(T.slot_unresolved);
+            if (COUNT) h.inc_t(T.slot_unresolved, -1);
         }
     }
     // SYN: src interface inbound
@@ -745,7 +786,7 @@ PG_HD void classify_q(const DevTableSet& T, const uint32_t* blobs, const DevTabl
             t[j] = e[j].tout;
             if (!run[j]) {
                 out[j] = verdict(kActFailure, T.slot_unresolved);
-                if (COUNT) h.inc(T.slot_unresolved);
+                if (COUNT) h.inc_t(T.slot_unresolved, -1);
             }
         }
         eval_step<Q, COUNT>(T, ev, t, run, false, h, out);
@@ -835,7 +876,7 @@ PG_HD void classify_node_q(const DevTableSet& T, const DevNode& N, const L& img,
             t[j] = e.tout;
             if (!run[j]) {
                 out[j] = verdict(kActFailure, T.slot_unresolved);
-                if (COUNT) h.inc(T.slot_unresolved);
+                if (COUNT) h.inc_t(T.slot_unresolved, -1);
             }
         }
         eval_step<Q, COUNT>(T, ev, t, run, false, h, out);

@@ -158,6 +158,8 @@ DeviceBuffers* dev_upload(const HostTableSet& h, std::string* err) {
     size_t o_ip = place(h.iphash.size() * 4);
     size_t o_nimg = place(h.node_img.size() * 4);
     size_t o_nx = place(h.node_cross.size() * 4);
+    size_t o_tw = place(h.hist.tabwin.size() * 4);
+    size_t o_cs = place(h.hist.cell_slot.size() * 4);
     std::vector<uint8_t> img(off, 0);
     auto put = [&](size_t o, const void* p, size_t n) {
         if (n) std::memcpy(img.data() + o, p, n);
@@ -169,6 +171,8 @@ DeviceBuffers* dev_upload(const HostTableSet& h, std::string* err) {
     put(o_ip, h.iphash.data(), h.iphash.size() * 4);
     put(o_nimg, h.node_img.data(), h.node_img.size() * 4);
     put(o_nx, h.node_cross.data(), h.node_cross.size() * 4);
+    put(o_tw, h.hist.tabwin.data(), h.hist.tabwin.size() * 4);
+    put(o_cs, h.hist.cell_slot.data(), h.hist.cell_slot.size() * 4);
     auto* b = new DeviceBuffers();
     b->blob = dev_alloc(off, err);
     if (!b->blob) {
@@ -200,6 +204,9 @@ DeviceBuffers* dev_upload(const HostTableSet& h, std::string* err) {
     v.node = h.node;
     v.node.img = h.node_img.empty() ? nullptr : (const uint32_t*)(base + o_nimg);
     v.node.cross = h.node_img.empty() ? nullptr : (const uint32_t*)(base + o_nx);
+    v.hist_cells = (uint32_t)h.hist.cell_slot.size();
+    v.hist_tabwin = v.hist_cells ? (const uint32_t*)(base + o_tw) : nullptr;
+    v.hist_cell_slot = v.hist_cells ? (const uint32_t*)(base + o_cs) : nullptr;
     b->host_tabs = h.tabs;
     b->host_blob_words = h.blob_words;
     b->host_blob_prefix = h.blob_prefix;
@@ -335,7 +342,7 @@ int dev_comm_allreduce_u64(void* const* comms, unsigned long long* const* bufs, 
 }
 
 constexpr int kBlock = 256;
-constexpr uint32_t kLdsHistMax = 16384;  // hit-counter cells kept in LDS (64 KiB): a window + 1
+constexpr uint32_t kLdsHistMax = kLdsHistCells + 2;  // hit-counter cells kept in LDS (64 KiB): a window + 2
 
 // Tuple streams are read once and verdicts written once: issued with the non-temporal
 // policy (A/B in one process with tools/sweep.py: +3-4 % on config 2; PG_NT_STREAM=0 builds
@@ -483,7 +490,7 @@ void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     uint32_t* hist = smem + (STAGE ? stage_words : 0u);
     // node kernels: the LDS histogram, when used, holds every slot (HistT<true>: no window test)
-    HistT<NODE, NODE && MODE == 1> h{nullptr, counters};
+    HistT<NODE, NODE && MODE == 1, NODE> h{nullptr, counters};
     DevTable tab0{};
     const uint32_t* blobs = T.blobs;
     // the node image: its LDS copy (at LDS address 0: LdsLoader) when staged, else global memory
@@ -514,14 +521,19 @@ void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
     // favours them: config 4's Zipf depth) and the extra cells its default-deny slot and its
     // last rule (a deny-the-rest / allow-all catch-all takes every unmatched packet: a single
     // global address would serialise them); node modes: "no ACL", "unresolved"
-    // node kernels over more slots than the histogram holds count with global atomics only
+    // node kernels over more slots than the full histogram holds count through per-table
+    // windows (device.hpp HistWindows; hist_cells + 2 = their cells) when the set has them, else
+    // with global atomics only
     const bool lds_hist = COUNT && (!NODE || hist_cells >= T.n_slots);
+    const bool twin = NODE && COUNT && !lds_hist && T.hist_cells != 0;
+    const bool has_hist = COUNT && (!NODE || lds_hist || twin);  // an LDS histogram was allocated
     const uint32_t wn = COUNT ? hist_cells : 0u;
     const uint32_t wbase = (MODE == 0 && wn < T.n_slots) ? min(tab0.rule_base, T.n_slots - wn) : 0u;
     const uint32_t xslot = MODE == 0 ? (tab0.dflt & kSlotMask) : T.slot_noacl;
     const uint32_t xslot1 = MODE == 0 ? (tab0.n_rules ? tab0.rule_base + tab0.n_rules - 1u : xslot) : T.slot_unresolved;
     if (COUNT) {
-        for (uint32_t i = threadIdx.x; i <= wn + 1u; i += BS) hist[i] = 0;
+        if (has_hist)
+            for (uint32_t i = threadIdx.x; i <= wn + (twin ? 2u : 1u); i += BS) hist[i] = 0;
         h.lds = lds_hist ? hist : nullptr;
         h.wbase = wbase;
         h.wn = wn;
@@ -536,6 +548,17 @@ void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
         if (MODE != 0 && PG_HOT_SLOT_NODE && !lds_hist && T.node_out >= 0) {
             const DevTable no = load_tab(T.tabs, T.node_out);
             if (no.n_rules) h.hot = no.rule_base + no.n_rules - 1u;
+        }
+        if (twin) {  // the windows {rb, n, cb, h} per table, after the cells (16-B aligned)
+            uint4* tw = reinterpret_cast<uint4*>(hist + ((wn + 2u + 1u + 3u) & ~3u));
+            const uint4* g = reinterpret_cast<const uint4*>(T.hist_tabwin);
+            for (uint32_t i = threadIdx.x; i < T.n_tables; i += BS) tw[i] = g[i];
+            h.twin = reinterpret_cast<const uint32_t*>(tw);
+            h.wlds = hist;
+            h.nr = T.n_rules;
+            // the register-counted hot slot (the node-output table's catch-all) goes to the extra
+            // cell after the windows' cells at the flush
+            h.hotcell = wn + 2u;
         }
     }
     if (STAGE || COUNT) __syncthreads();
@@ -647,10 +670,12 @@ void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
     if (COUNT) {
         h.flush_hot();
         __syncthreads();
-        for (uint32_t i = threadIdx.x; i <= wn + 1u; i += BS) {
+        for (uint32_t i = threadIdx.x; has_hist && i <= wn + (twin ? 2u : 1u); i += BS) {
             const uint32_t v = hist[i];
+            const uint32_t slot = twin ? (i < wn + 2u ? T.hist_cell_slot[i] : h.hot)
+                                       : (i < wn ? wbase + i : (i == wn ? xslot : xslot1));
 #if !defined(PG_PROBE_NOFLUSH)  // measurement build only: the histogram is not flushed
-            if (v) atomicAdd(&counters[i < wn ? wbase + i : (i == wn ? xslot : xslot1)], (unsigned long long)v);
+            if (v) atomicAdd(&counters[slot], (unsigned long long)v);
 #endif
         }
     }
@@ -859,14 +884,14 @@ static int grid_resident(K kernel, int bs, size_t lds, uint64_t items, uint32_t 
 template <int MODE, bool COUNT, bool VEC, int STAGE, bool NODE, int BS>
 static void launch_bs(const DevTableSet& T, const Tuning& tu, int t, const uint32_t* src, const uint32_t* dst, const uint16_t* sport,
                       const uint16_t* dport, const uint8_t* proto, uint64_t n, uint32_t* out,
-                      unsigned long long* counters, hipStream_t st, size_t hist, uint32_t stage, uint64_t items) {
+                      unsigned long long* counters, hipStream_t st, size_t hist, uint32_t cells, uint32_t stage,
+                      uint64_t items) {
     auto k = k_classify<MODE, COUNT, VEC, STAGE, NODE, BS>;
     // SINGLE over an LDS-staged FD table without counters: two resident workgroups per CU, not
     // the three LDS would allow (A/B on MI355X, config 2: 541-546 vs 533-535 Gpps, repeated
     // three times; with counters no difference): fewer streams in flight per CU contend less
     const uint32_t bpc = tu.blocks_per_cu ? tu.blocks_per_cu : (MODE == 0 && (STAGE & 7) == 4 && !COUNT ? 2u : 0u);
     const size_t lds = hist + (size_t)stage * 4;
-    const uint32_t cells = hist ? (uint32_t)(hist / 4 - 2) : 0u;  // window cells (+ the two extra ones)
     hipLaunchKernelGGL(k, dim3(grid_resident(k, BS, lds, items, bpc)), dim3(BS), lds, st, T, t, src, dst, sport, dport,
                        proto, n, out, counters, stage, cells);
 }
@@ -876,7 +901,8 @@ static void launch_bs(const DevTableSet& T, const Tuning& tu, int t, const uint3
 template <int MODE, bool COUNT, bool VEC, int STAGE, bool NODE>
 static void launch_one(const DevTableSet& T, const Tuning& tu, int t, const uint32_t* src, const uint32_t* dst, const uint16_t* sport,
                        const uint16_t* dport, const uint8_t* proto, uint64_t n, uint32_t* out,
-                       unsigned long long* counters, hipStream_t st, size_t hist, uint32_t stage, uint64_t items) {
+                       unsigned long long* counters, hipStream_t st, size_t hist, uint32_t cells, uint32_t stage,
+                       uint64_t items) {
     if constexpr (STAGE) {
         // 512 (A/B on MI355X: SINGLE with counters +14 % over 1024 at config 2; without
         // counters +2.5 % since SINGLE classifies one tuple per chunk, v15; config 4 over its
@@ -886,13 +912,13 @@ static void launch_one(const DevTableSet& T, const Tuning& tu, int t, const uint
                                                                                                                 : 512u);
         if (bs == 1024u)
             return launch_bs<MODE, COUNT, VEC, STAGE, NODE, 1024>(T, tu, t, src, dst, sport, dport, proto, n, out,
-                                                                  counters, st, hist, stage, items);
+                                                                  counters, st, hist, cells, stage, items);
         if (bs == 512u)
             return launch_bs<MODE, COUNT, VEC, STAGE, NODE, 512>(T, tu, t, src, dst, sport, dport, proto, n, out,
-                                                                 counters, st, hist, stage, items);
+                                                                 counters, st, hist, cells, stage, items);
     }
     launch_bs<MODE, COUNT, VEC, STAGE, NODE, 256>(T, tu, t, src, dst, sport, dport, proto, n, out, counters, st, hist,
-                                                  stage, items);
+                                                  cells, stage, items);
 }
 
 // SINGLE over a non-FD table: the blob in LDS (STAGE 1), its root in LDS (2) or all in HBM (0);
@@ -900,28 +926,43 @@ static void launch_one(const DevTableSet& T, const Tuning& tu, int t, const uint
 template <int MODE, bool COUNT, bool VEC, int NODST>
 static void launch_generic(const DevTableSet& T, const Tuning& tu, int t, const uint32_t* src, const uint32_t* dst,
                            const uint16_t* sport, const uint16_t* dport, const uint8_t* proto, uint64_t n,
-                           uint32_t* out, unsigned long long* counters, hipStream_t st, size_t hist, uint32_t words,
-                           uint32_t root_words, uint64_t items) {
+                           uint32_t* out, unsigned long long* counters, hipStream_t st, size_t hist, uint32_t cells,
+                           uint32_t words, uint32_t root_words, uint64_t items) {
     const DevTable& hd = T.host_tabs[t];
     if (!(hd.fsk & kFlagLinear) && words && words <= tu.stage_max_words)
         launch_one<MODE, COUNT, VEC, 1 + NODST, false>(T, tu, t, src, dst, sport, dport, proto, n, out, counters, st,
-                                                       hist, words, items);
+                                                       hist, cells, words, items);
     else if (!(hd.fsk & kFlagLinear) && words && root_words <= tu.stage_root_max_words)
         launch_one<MODE, COUNT, VEC, 2 + NODST, false>(T, tu, t, src, dst, sport, dport, proto, n, out, counters, st,
-                                                       hist, root_words, items);
+                                                       hist, cells, root_words, items);
     else
         launch_one<MODE, COUNT, VEC, 0 + NODST, false>(T, tu, t, src, dst, sport, dport, proto, n, out, counters, st,
-                                                       hist, 0, items);
+                                                       hist, cells, 0, items);
 }
 
 template <int MODE, bool COUNT, bool VEC>
 static void launch_classify(const DevTableSet& T, const Tuning& tu, int t, const uint32_t* src, const uint32_t* dst,
                             const uint16_t* sport, const uint16_t* dport, const uint8_t* proto, uint64_t n,
                             uint32_t* out, unsigned long long* counters, hipStream_t st) {
-    // hit-counter LDS histogram: every slot + 1 cell, or (more slots than fit) a window of
-    // hist_window cells + 1 (k_classify)
-    const uint32_t cells = T.n_slots <= kLdsHistMax - 2u ? T.n_slots : std::min(tu.hist_window, kLdsHistMax - 2u);
-    const size_t hist = COUNT ? ((size_t)cells + 2u) * 4 : 0;
+    // hit-counter LDS histogram (k_classify): every slot + 2 cells; or (more slots than fit) a
+    // SINGLE table's window of hist_window cells + 2; or the node set's per-table windows
+    // (HistWindows: their cells, one for the register-counted hot slot, then the windows
+    // themselves, 16 B per table); a node set without windows counts with global atomics only
+    const bool node = MODE != 0 && tu.node_path && T.node.img;
+    uint32_t cells = 0;
+    size_t hist = 0;
+    if (COUNT) {
+        if (T.n_slots <= kLdsHistMax - 2u) {
+            cells = T.n_slots;
+            hist = ((size_t)cells + 2u) * 4;
+        } else if (!node) {
+            cells = std::min(tu.hist_window, kLdsHistMax - 2u);
+            hist = ((size_t)cells + 2u) * 4;
+        } else if (T.hist_cells) {
+            cells = T.hist_cells - 2u;
+            hist = (((size_t)T.hist_cells + 1u + 3u) & ~(size_t)3) * 4 + (size_t)T.n_tables * 16;
+        }
+    }
     const uint64_t items = VEC ? (n + PG_TPL - 1) / PG_TPL : n;
     if constexpr (MODE == 0) {
         const DevTable& hd = T.host_tabs[t];
@@ -930,32 +971,32 @@ static void launch_classify(const DevTableSet& T, const Tuning& tu, int t, const
         const uint32_t prefix = T.host_blob_prefix[t];
         if ((hd.fsk & kFlagFD) && words <= tu.stage_max_words)  // FD blob in LDS, no dst stream
             launch_one<MODE, COUNT, VEC, 4, false>(T, tu, t, src, dst, sport, dport, proto, n, out, counters, st, hist,
-                                                   words, items);
+                                                   cells, words, items);
         else if ((hd.fsk & kFlagFD) && prefix <= tu.stage_root_max_words)  // its prefix in LDS, the rest in HBM
             launch_one<MODE, COUNT, VEC, 5, false>(T, tu, t, src, dst, sport, dport, proto, n, out, counters, st, hist,
-                                                   prefix, items);
+                                                   cells, prefix, items);
         else if (hd.fsk & kFlagDstFree)  // no rule tests dst: the dst stream is not read
             launch_generic<MODE, COUNT, VEC, 8>(T, tu, t, src, dst, sport, dport, proto, n, out, counters, st, hist,
-                                                words, root_words, items);
+                                                cells, words, root_words, items);
         else
             launch_generic<MODE, COUNT, VEC, 0>(T, tu, t, src, dst, sport, dport, proto, n, out, counters, st, hist,
-                                                words, root_words, items);
-    } else if (tu.node_path && T.node.img) {
+                                                cells, words, root_words, items);
+    } else if (node) {
         // the image with its common-row section when that fits the LDS budget next to the
         // histogram, else the base image (STAGE 1), else the image is read from HBM / L2
         if (T.node.cmap && hist + (size_t)T.node.img_words * 4 <= tu.node_common_lds_max &&
             T.node.img_words <= tu.node_stage_max_words + kCommonStageExtraWords)
             launch_one<MODE, COUNT, VEC, 3, true>(T, tu, t, src, dst, sport, dport, proto, n, out, counters, st, hist,
-                                                  T.node.img_words, items);
+                                                  cells, T.node.img_words, items);
         else if (T.node.img_words_base <= tu.node_stage_max_words)
             launch_one<MODE, COUNT, VEC, 1, true>(T, tu, t, src, dst, sport, dport, proto, n, out, counters, st, hist,
-                                                  T.node.img_words_base, items);
+                                                  cells, T.node.img_words_base, items);
         else
             launch_one<MODE, COUNT, VEC, 0, true>(T, tu, t, src, dst, sport, dport, proto, n, out, counters, st, hist,
-                                                  0, items);
+                                                  cells, 0, items);
     } else {
-        launch_one<MODE, COUNT, VEC, 0, false>(T, tu, t, src, dst, sport, dport, proto, n, out, counters, st, hist, 0,
-                                               items);
+        launch_one<MODE, COUNT, VEC, 0, false>(T, tu, t, src, dst, sport, dport, proto, n, out, counters, st, hist,
+                                               cells, 0, items);
     }
 }
 
