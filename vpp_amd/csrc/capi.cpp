@@ -168,9 +168,7 @@ void pg_destroy(pg_ctx* ctx) {
 // process defaults: contexts created afterwards start from them
 int pg_set_tuning(const char* key, int value) {
     if (!key) return PG_EINVAL;
-    static std::mutex mu;
-    std::lock_guard<std::mutex> lk(mu);
-    return tuning_set(default_tuning(), key, value) == 0 ? PG_OK : PG_EINVAL;
+    return default_tuning_set(key, value) == 0 ? PG_OK : PG_EINVAL;
 }
 
 int pg_ctx_set_tuning(pg_ctx* ctx, const char* key, int value) {

@@ -22,6 +22,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <atomic>
 #include <type_traits>
 #include <cstdio>
 #include <cstdlib>
@@ -847,15 +848,17 @@ constexpr uint32_t kCommonStageExtraWords = 8192;  // the section may take the i
 // CUs of the current device (per device: contexts on different GPUs share the process)
 static uint32_t num_cus() {
     constexpr int kMaxDev = 64;
-    static uint32_t cus[kMaxDev] = {};
+    static std::atomic<uint32_t> cus[kMaxDev] = {};  // contexts on several threads may launch at once
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDev) return 256;
-    if (!cus[dev]) {
+    uint32_t c = cus[dev].load(std::memory_order_relaxed);
+    if (!c) {
         hipDeviceProp_t p;
-        cus[dev] = (hipGetDeviceProperties(&p, dev) == hipSuccess && p.multiProcessorCount > 0)
-                       ? (uint32_t)p.multiProcessorCount : 256u;
+        c = (hipGetDeviceProperties(&p, dev) == hipSuccess && p.multiProcessorCount > 0) ? (uint32_t)p.multiProcessorCount
+                                                                                       : 256u;
+        cus[dev].store(c, std::memory_order_relaxed);
     }
-    return cus[dev];
+    return c;
 }
 
 static int grid_for(uint64_t items, uint32_t blocks_per_cu = 0) {

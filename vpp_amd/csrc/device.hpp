@@ -179,7 +179,10 @@ struct Tuning {
 // tables are compiled (the context recompiles on its next use).
 int tuning_set(Tuning& t, const std::string& key, int value, bool* compiler = nullptr);
 int tuning_get(const Tuning& t, const std::string& key, int* value);
-Tuning& default_tuning();  // process defaults (contexts copy them when created)
+// process defaults (contexts copy them when created), behind one lock: pg_set_tuning may race
+// pg_create on another thread
+Tuning default_tuning();
+int default_tuning_set(const std::string& key, int value);
 
 // fastpath.cpp: classification blob of one table (false = does not fit the budgets). When
 // `an` is given it receives the table's class analysis for build_node.

@@ -4,6 +4,7 @@
 #include "classify.hpp"
 
 #include <algorithm>
+#include <mutex>
 #include <set>
 
 #include "../../include/policygpu.h"
@@ -11,9 +12,25 @@
 namespace pg {
 
 // ---- tuning --------------------------------------------------------------------------------
-Tuning& default_tuning() {
+namespace {
+std::mutex& defaults_mu() {
+    static std::mutex mu;
+    return mu;
+}
+Tuning& defaults() {
     static Tuning t;
     return t;
+}
+}  // namespace
+
+Tuning default_tuning() {
+    std::lock_guard<std::mutex> lk(defaults_mu());
+    return defaults();
+}
+
+int default_tuning_set(const std::string& key, int value) {
+    std::lock_guard<std::mutex> lk(defaults_mu());
+    return tuning_set(defaults(), key, value);
 }
 
 namespace {
