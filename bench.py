@@ -159,7 +159,8 @@ def main():
 
     bpt, fields = bytes_per_tuple(w)
     achieved = n * bpt / (kern_ms * 1e-3) / 1e9
-    traffic, traffic_src = pmc_traffic(a.config, n, (a.counters and not w.counters) or bool(a.rules))
+    label = "%d" % a.config + ("r%d" % a.rules if a.rules else "")
+    traffic, traffic_src = pmc_traffic(label, n, a.counters and not w.counters)
     line = {
         "metric": METRIC, "value": round(mpps, 1), "unit": "Mpps", "n_gpus": world, "steps": a.steps,
         "warmup": a.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True, "scaling": a.scaling,
@@ -403,15 +404,16 @@ def classifier(w, per_table):
     return "node: %s" % json.dumps(ns)
 
 
-def pmc_traffic(config, n, other_shape):
+def pmc_traffic(label, n, other_shape):
     """HBM bytes per classify launch from the committed rocprofv3 PMC summary of this config
-    (profiles/rNN_*_config<C>_pmc.json, FETCH_SIZE/WRITE_SIZE passes, gfx950-corrected by
-    tools/prof_summary.py), scaled to this launch's tuple count; None when there is none."""
+    (profiles/rNN_*_config<label>_pmc.json, label = C or CrM for config C at M rules,
+    FETCH_SIZE/WRITE_SIZE passes, gfx950-corrected by tools/prof_summary.py), scaled to this
+    launch's tuple count; None when there is none."""
     import glob
     import re
     # newest round / version first by number (r01_v12 after r01_v9)
     nat = lambda p: [int(x) if x.isdigit() else x for x in re.split(r"(\d+)", os.path.basename(p))]
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_config%d_pmc.json" % config)), key=nat)
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_config%s_pmc.json" % label)), key=nat)
     if not files or other_shape:  # the committed summary is of the default shape only
         return None, None
     with open(files[-1]) as f:

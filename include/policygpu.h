@@ -164,7 +164,9 @@ int pg_ctx_device(const pg_ctx* ctx);
  * 12), "candi" (1/0: candidates inline in the 8-B trie entries of HBM-resident candidate tables
  * no live rule of which tests dst, default 1), "fd" (1/0: fixed-depth form of dst-independent
  * cross-product tables, default 1), "node_common" (1/0: common-row section of node
- * images, default 1), "pair" (1/0: the PAIR structure -- src x dst classes, then x key classes
+ * images, default 1), "node_list_words" (node dst records -- the dst-specific rules a node
+ * cross entry must still test -- up to this many words go into the node image, so a launch that
+ * stages the image walks them in LDS; default 4096, 0 = never), "pair" (1/0: the PAIR structure -- src x dst classes, then x key classes
  * -- for tables the cross product cannot take, default 1; 0 = candidate lists; 2 = wherever it
  * fits, for tests).
  * pg_ctx_set_tuning sets one context's knob; pg_set_tuning sets the process default that
@@ -257,6 +259,9 @@ int pg_node_stats(pg_ctx* ctx, uint32_t* ip_classes, uint32_t* key_classes, uint
  * the covered (table, IPv4 class) pairs read the table's common row from the image instead of
  * the cross table (0 when the section was not built); PG_ENOENT when there is no node */
 int pg_node_common_stats(pg_ctx* ctx, uint64_t* base_image_bytes, uint64_t* common_pairs, uint64_t* pairs);
+/* the node classifier's dst records (the dst-specific rules its cross entries still test): their
+ * bytes, and whether a copy ends the node image (tuning "node_list_words"); PG_ENOENT: no node */
+int pg_node_list_stats(pg_ctx* ctx, uint64_t* record_bytes, int* in_image);
 /* reference-shaped linear-scan kernel (K1) on one table, for validation and comparison */
 int pg_classify_linear(pg_ctx* ctx, int table_id, const pg_tuple_soa* tuples, uint64_t n, uint32_t* out,
                        void* hip_stream);

@@ -179,6 +179,31 @@ def test_config3_cluster_node_path():
     assert np.array_equal(got >> 30, conn.astype(np.uint32)) and np.array_equal(got & 0x3FFFFFFF, cslot)
     got0 = e.debug_classify_host(MODE_CONN, -1, src, dst, sport, dport, proto, node=True, common=False)
     assert np.array_equal(got0, got)
+    # the global table's dst-specific rules: dst records, a copy at the end of the image
+    assert ns["list_record_bytes"] > 0 and ns["list_records_in_image"], ns
+
+
+def test_node_dst_records_in_image_or_cross():
+    """Node dst records read from the image copy (default) and from the cross array
+    (node_list_words=0: no copy) classify the same, and equal the oracle."""
+    w = W.config3(0, n_tuples=1 << 10, n_ns=4)
+    src, dst, sport, dport, proto = gen.gen_tuples(30001, **w.gen)
+    ns = w.engine.node_stats()
+    assert ns["list_records_in_image"] and ns["image_bytes"] >= ns["list_record_bytes"], ns
+    a = w.engine.debug_classify_host(MODE_PERPOD, -1, src, dst, sport, dport, proto, node=True)
+    c = w.engine.debug_classify_host(MODE_CONN, -1, src, dst, sport, dport, proto, node=True)
+    assert _capi.lib.pg_set_tuning(b"node_list_words", 0) == 0
+    try:
+        w2 = W.config3(0, n_tuples=1 << 10, n_ns=4)
+        ns2 = w2.engine.node_stats()
+        assert not ns2["list_records_in_image"] and ns2["image_bytes"] == ns["image_bytes"] - ns["list_record_bytes"]
+        assert np.array_equal(w2.engine.debug_classify_host(MODE_PERPOD, -1, src, dst, sport, dport, proto, node=True), a)
+        assert np.array_equal(w2.engine.debug_classify_host(MODE_CONN, -1, src, dst, sport, dport, proto, node=True), c)
+    finally:
+        assert _capi.lib.pg_set_tuning(b"node_list_words", 4096) == 0
+    wd = World(w.engine, w.local_ifs, w.node_if)
+    act, slot = wd.perpod(src, dst, dport, proto, threads=8)
+    assert np.array_equal(a >> 30, act.astype(np.uint32)) and np.array_equal(a & 0x3FFFFFFF, slot)
 
 
 def test_common_rows_disabled():
@@ -193,7 +218,8 @@ def test_common_rows_disabled():
     try:
         e2, local2, pod_ips2 = topology(random.Random(77))
         ns2 = e2.node_stats()
-        assert ns2["common_row_pairs"] == 0 and ns2["image_bytes"] == ns2["base_image_bytes"]
+        recs = ns2["list_record_bytes"] if ns2["list_records_in_image"] else 0
+        assert ns2["common_row_pairs"] == 0 and ns2["image_bytes"] == ns2["base_image_bytes"] + recs
         assert np.array_equal(e2.debug_classify_host(MODE_CONN, -1, *tup, node=True), on)
     finally:
         assert _capi.lib.pg_set_tuning(b"node_common", 1) == 0

@@ -3,6 +3,7 @@
 # Builds: make -C vpp_amd/csrc variant V=name DEFS="-DPG_...=..." -> vpp_amd/libpolicygpu_name.so
 # Configs: 3, 5c (with counters), r10000 (config 2 at 10k rules), ...
 #   gpurun -- bash tools/ab.sh TAG "libA libB" "3 5c 6" [pytest paths]
+# PRE="key=v ..." (environment): compiler knobs set before the tables are built (sweep.py --pre)
 set -o pipefail
 TAG=${1:-ablib}; LIBS=${2:-libpolicygpu.so}; CONFIGS=${3:-3}; TESTS=${4:-}
 R=$(pwd)
@@ -21,7 +22,8 @@ for lib in $LIBS; do
         cnt=""; case $c in *c) cnt="--counters";; esac
         extra=""; case $c in r*) extra="--rules ${c#r}"; c=2;; esac
         step sweep $lib config $c $cnt $extra
-        VPP_AMD_LIB=$R/vpp_amd/$lib timeout -k 10 200 python tools/sweep.py --config ${c%c} --rounds 3 --reps 5 $cnt \
+        pre=""; for kv in ${PRE:-}; do pre="$pre --pre $kv"; done
+        VPP_AMD_LIB=$R/vpp_amd/$lib timeout -k 10 200 python tools/sweep.py --config ${c%c} --rounds 3 --reps 5 $cnt $pre \
             >> "$O/sweep.jsonl" 2> "$O/sweep.err" || { tail -20 "$O/sweep.err"; exit 1; }
     done
 done
@@ -29,6 +31,6 @@ done
 python -c "
 import json
 for l in open('$O/sweep.jsonl'):
-    d=json.loads(l); print(d['lib'], d['config'], d['counters'], d['ms'], d['gpps'])
+    d=json.loads(l); print(d['lib'], d['config'], d['counters'], d['pre'], d['ms'], d['gpps'], d.get('out_sha'))
 "
 step done

@@ -90,7 +90,7 @@ def main():
         other_raw = f_raw - stream_raw
         traffic = 2 * stream_raw + other_raw + w_raw
         summary = {
-            "config": int(cfg), "kernel": kname, "launches_sampled": len(fetch[kname]),
+            "config": int(cfg) if cfg.isdigit() else cfg, "kernel": kname, "launches_sampled": len(fetch[kname]),
             "tuples_per_launch": n, "algorithmic_bytes_per_launch": algo,
             "fetch_size_raw_bytes": round(f_raw), "write_size_bytes": round(w_raw),
             "fetch_stream_bytes_corrected": round(2 * stream_raw),

@@ -85,7 +85,9 @@ def main():
         extra = {"blob": e.table_stats(w.table_id)} if w.mode == 0 and i == 0 else {}
         print(json.dumps({"lib": name, "config": a.config, "counters": a.counters, "pre": a.pre, "ns": a.ns, "rules": a.rules, **dict(zip(keys, combo)), "ms": round(ms, 4),
                           "gpps": round(n / ms / 1e6, 1), "GBps": round(n * bpt / ms / 1e6, 1),
-                          "same_output": bool(torch.equal(outs[i], ref)), **extra}), flush=True)
+                          "same_output": bool(torch.equal(outs[i], ref)),
+                          "out_sha": __import__("hashlib").sha1(outs[i].cpu().numpy().tobytes()).hexdigest()[:12],
+                          **extra}), flush=True)
 
 
 if __name__ == "__main__":

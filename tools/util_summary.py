@@ -50,7 +50,7 @@ def main():
         cfg = os.path.basename(bench)[len("bench_c"):-len(".json")]
         line = json.loads(open(bench).read().strip().splitlines()[-1])
         n = line["config"]["tuples_per_gpu"]
-        res = {"config": int(cfg), "tuples_per_launch": n, "passes": {}}
+        res = {"config": int(cfg) if cfg.isdigit() else cfg, "tuples_per_launch": n, "passes": {}}
         acc = {}
         for name, ds in passes(src, cfg).items():
             avg = {k: sum(d.get(k, 0.0) for d in ds) / len(ds) for k in ds[0]}

@@ -720,10 +720,23 @@ int pg_node_common_stats(pg_ctx* ctx, uint64_t* base_image_bytes, uint64_t* comm
     for (size_t t = 0; t < h.tabs.size(); t++)
         if (h.node_img[h.node.tabinfo + 4 * t + 1] >> 31) covered++;
     if (h.node.cmap)
-        for (size_t i = h.node.cmap; i < h.node.img_words; i++) common += (uint64_t)__builtin_popcount(h.node_img[i]);
+        for (size_t i = h.node.cmap; i < (h.node.lrec ? h.node.lrec : h.node.img_words); i++) common += (uint64_t)__builtin_popcount(h.node_img[i]);
     if (base_image_bytes) *base_image_bytes = (uint64_t)h.node.img_words_base * 4;
     if (common_pairs) *common_pairs = common;
     if (pairs) *pairs = covered * h.node.n_ipc;
+    return PG_OK;
+    GUARD_END(ctx)
+}
+
+int pg_node_list_stats(pg_ctx* ctx, uint64_t* record_bytes, int* in_image) {
+    if (!ctx) return PG_EINVAL;
+    GUARD_BEGIN
+    Engine& E = ctx->eng;
+    if (!E.compiled) E.compile();
+    const HostTableSet& h = E.host;
+    if (h.node_img.empty()) return fail(ctx, PG_ENOENT, "no node classifier (disabled or over budget)");
+    if (record_bytes) *record_bytes = ((uint64_t)h.node_cross.size() - h.node.rec0) * 4;
+    if (in_image) *in_image = h.node.lrec != 0;
     return PG_OK;
     GUARD_END(ctx)
 }

@@ -600,27 +600,35 @@ struct NodeEval {
             pend[j] = false;
             pos[j] = 0;
             if (!on[j]) continue;
+#if defined(PG_PROBE_NOLIST)  // measurement build only: dst records not walked
+            w[j] &= ~kNodeList;
+#endif
             pend[j] = (w[j] & kNodeList) != 0u;
             pos[j] = (w[j] & kNodeRecMask) << 2;
         }
-        // dst records until the first match (every list ends with a match-all record)
-        for (;;) {
-            bool more = false;
-            PG_UNROLL
-            for (int j = 0; j < Q; j++) more |= pend[j];
-            if (!more) break;
-            PG_UNROLL
-            for (int j = 0; j < Q; j++) {
-                if (!pend[j]) continue;
-                const W4 r = X.u4(pos[j]);
-                if (rec_match(r, b[j], k[j])) {
-                    w[j] = r.w;
-                    pend[j] = false;
-                } else {
-                    pos[j] += 4u;
+        // dst records until the first match (every list ends with a match-all record): from the
+        // image (N.lrec, uniform) or the cross array
+        auto walk = [&](const auto& R, uint32_t delta) {
+            for (;;) {
+                bool more = false;
+                PG_UNROLL
+                for (int j = 0; j < Q; j++) more |= pend[j];
+                if (!more) break;
+                PG_UNROLL
+                for (int j = 0; j < Q; j++) {
+                    if (!pend[j]) continue;
+                    const W4 r = R.u4(pos[j] + delta);
+                    if (rec_match(r, b[j], k[j])) {
+                        w[j] = r.w;
+                        pend[j] = false;
+                    } else {
+                        pos[j] += 4u;
+                    }
                 }
             }
-        }
+        };
+        if (N.lrec) walk(img, N.lrec - N.rec0);
+        else walk(X, 0u);
         bool anyfb = false;
         PG_UNROLL
         for (int j = 0; j < Q; j++) anyfb |= fb[j];

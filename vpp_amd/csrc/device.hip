@@ -375,8 +375,9 @@ __device__ __forceinline__ void stream_store(V v, V* p) {
 // NODE (PERPOD / CONN): the node classifier; STAGE then copies the node image into LDS.
 //
 // Stream pipelining (PG_PREFETCH): 1 = the next group's loads are issued at the top of each
-// iteration; 2 = (NODE) issued right after the first cross-entry gather of the iteration, so
-// waiting for that gather does not also wait for them (vmcnt retires in issue order); 0 = none;
+// iteration; 2 = (NODE) issued right after the cross-entry gathers of the group's first (or,
+// PG_HOOK_LAST, last) chunk, so waiting for those gathers does not also wait for them (vmcnt
+// retires in issue order); 3 = after the group's classification; 0 = none;
 // -1 (default) = per mode: none for SINGLE over an LDS-staged blob (all lookups in LDS,
 // occupancy hides the stream), top-of-iteration for SINGLE over a blob in HBM and for PERPOD /
 // CONN (tools/sweep.py A/B on MI355X).
@@ -416,6 +417,12 @@ __device__ __forceinline__ void stream_store(V v, V* p) {
 #endif
 #ifndef PG_PREFETCH_FD  // STAGE 4 / 5: stream prefetch of the next group (see PG_PREFETCH)
 #define PG_PREFETCH_FD 0
+#endif
+#ifndef PG_PF_DEPTH  // launches with stream prefetch: groups loaded ahead (1 or 2)
+#define PG_PF_DEPTH 1
+#endif
+#ifndef PG_HOOK_LAST  // PF 2: the loads issued after the gathers of the group's last chunk (else its first)
+#define PG_HOOK_LAST 0
 #endif
 #ifndef PG_TPL  // tuples per lane per loop iteration (4 or 8)
 #define PG_TPL 4
@@ -596,20 +603,34 @@ void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
     // default: SINGLE over an LDS-staged blob none, SINGLE over a blob in HBM (STAGE 0 / 2) and
     // the node modes the next group at the top of the iteration (A/B on MI355X, config 4 with
     // four tuples per chunk: 172.9 vs 169.3 Gpps)
-    constexpr int PF = FD ? PG_PREFETCH_FD
+    constexpr int PF0 = FD ? PG_PREFETCH_FD
                           : (PG_PREFETCH >= 0 ? PG_PREFETCH
                                               : ((MODE == 0 && STAGE != 0 && STAGE != 2) ||
                                                  (NODE && MODE == 2 && COUNT && kernel_wpe<MODE, COUNT, NODE>() >= 8)
                                                      ? 0 : 1));
+    constexpr int PF = (!NODE && PF0 == 2) ? 1 : PF0;  // (only node kernels have the gather hook)
+    // PD = 2 (PG_PF_DEPTH): the loads run two groups ahead (group q + 2 * stride is
+    // loaded while group q is classified). PF 3: the loads are issued after the group's
+    // classification (its gathers waited for), just before its verdict store. Vector-memory
+    // operations retire in issue order (MI355X_MICROARCH.md, vmcnt), so a cross-table gather
+    // issued after a stream load waits for that load too.
+    constexpr int PD = PF ? PG_PF_DEPTH : 1;
+    Group ahead{};
     if (PF && q < nfull) cur = load(q);
+    if (PD == 2 && q + stride < nfull) ahead = load(q + stride);
     while (q < nfull) {
-        const uint64_t qn = q + stride;
-        Group nxt = cur;
+        const uint64_t qn = q + stride, qa = PD == 2 ? qn + stride : qn;  // qa: the group loaded now
+        Group nxt = PD == 2 ? ahead : cur;
         if (!PF) cur = load(q);
-        const bool late = NODE && PF == 2;
-        if (PF && !late && qn < nfull) nxt = load(qn);
+        auto issue = [&]() {
+            if (qa < nfull) {
+                if constexpr (PD == 2) ahead = load(qa);
+                else nxt = load(qa);
+            }
+        };
+        if (PF == 1) issue();
         [[maybe_unused]] auto hook = [&]() {
-            if (late && qn < nfull) nxt = load(qn);
+            if (PF == 2) issue();
         };
         uint32_t sv[P], dv[P], spv[P], dpv[P], prv[P], o[P];
 #pragma unroll
@@ -639,7 +660,7 @@ void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
                 if constexpr (STAGE == 4) classify_fd_q<COUNT, QC>(T, LdsLoader{}, LdsLoader{}, tab0, cs, cdp, cpr, h, co);
                 else classify_fd_q<COUNT, QC>(T, LdsLoader{}, DevLoader{fd_blob}, tab0, cs, cdp, cpr, h, co);
             } else if constexpr (NODE) {
-                if (c == 0)
+                if (c == (PG_HOOK_LAST ? P - QC : 0))
                     classify_node_q<MODE, COUNT, QC, STAGE && PG_PRED, STAGE == 3>(T, T.node, img, cs, cd, csp, cdp, cpr, h, co, hook);
                 else
                     classify_node_q<MODE, COUNT, QC, STAGE && PG_PRED, STAGE == 3>(T, T.node, img, cs, cd, csp, cdp, cpr, h, co);
@@ -650,6 +671,7 @@ void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
             for (int j = 0; j < QC; j++) o[c + j] = co[j];
         }
 #endif
+        if (PF == 3) issue();
         Words<P> ow;
 #pragma unroll
         for (int j = 0; j < P; j++) ow.w[j] = o[j];
@@ -985,18 +1007,30 @@ static void launch_classify(const DevTableSet& T, const Tuning& tu, int t, const
             launch_generic<MODE, COUNT, VEC, 0>(T, tu, t, src, dst, sport, dport, proto, n, out, counters, st, hist,
                                                 cells, words, root_words, items);
     } else if (node) {
-        // the image with its common-row section when that fits the LDS budget next to the
-        // histogram, else the base image (STAGE 1), else the image is read from HBM / L2
-        if (T.node.cmap && hist + (size_t)T.node.img_words * 4 <= tu.node_common_lds_max &&
-            T.node.img_words <= tu.node_stage_max_words + kCommonStageExtraWords)
-            launch_one<MODE, COUNT, VEC, 3, true>(T, tu, t, src, dst, sport, dport, proto, n, out, counters, st, hist,
-                                                  cells, T.node.img_words, items);
-        else if (T.node.img_words_base <= tu.node_stage_max_words)
-            launch_one<MODE, COUNT, VEC, 1, true>(T, tu, t, src, dst, sport, dport, proto, n, out, counters, st, hist,
-                                                  cells, T.node.img_words_base, items);
-        else
+        // the image with its common-row section and dst records when that fits the LDS budget
+        // next to the histogram, else without the records (the kernel then reads them from the
+        // cross array: lrec cleared), else the base image (STAGE 1), else the image is read from
+        // HBM / L2
+        DevTableSet Tn = T;
+        const uint32_t all = T.node.img_words, norec = T.node.lrec ? T.node.lrec : all;
+        auto fits = [&](uint32_t w) {
+            return hist + (size_t)w * 4 <= tu.node_common_lds_max && w <= tu.node_stage_max_words + kCommonStageExtraWords;
+        };
+        if (T.node.cmap && (fits(all) || fits(norec))) {
+            const uint32_t w = fits(all) ? all : norec;
+            if (w < all) Tn.node.lrec = 0;
+            launch_one<MODE, COUNT, VEC, 3, true>(Tn, tu, t, src, dst, sport, dport, proto, n, out, counters, st, hist,
+                                                  cells, w, items);
+        } else if (T.node.img_words_base <= tu.node_stage_max_words) {
+            // (without a common-row section the records follow the base image directly)
+            const bool recs = !T.node.cmap && T.node.lrec && all <= tu.node_stage_max_words;
+            if (!recs) Tn.node.lrec = 0;
+            launch_one<MODE, COUNT, VEC, 1, true>(Tn, tu, t, src, dst, sport, dport, proto, n, out, counters, st, hist,
+                                                  cells, recs ? all : T.node.img_words_base, items);
+        } else {
             launch_one<MODE, COUNT, VEC, 0, true>(T, tu, t, src, dst, sport, dport, proto, n, out, counters, st, hist,
                                                   cells, 0, items);
+        }
     } else {
         launch_one<MODE, COUNT, VEC, 0, false>(T, tu, t, src, dst, sport, dport, proto, n, out, counters, st, hist,
                                                cells, 0, items);

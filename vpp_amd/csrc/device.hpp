@@ -69,8 +69,8 @@ constexpr uint32_t kNodePairFlag = 1u << 30;
 struct DevNode {
     const uint32_t* img;   // null: no node classifier (the per-table path runs)
     const uint32_t* cross;
-    uint32_t img_words;    // whole image (with the common-row section when cmap != 0)
-    uint32_t img_words_base;  // image without the common-row section
+    uint32_t img_words;    // whole image (with the common-row section when cmap != 0, and the dst records)
+    uint32_t img_words_base;  // image without the common-row section and the dst records
     uint32_t cmap;         // word offset of the common-row bitmap in img, 0 = none
     uint32_t ip_s1, key_root, key_k1;
     // fixed-depth tries (blobwalk.hpp node_child_byte): a leaf points at its class's self word
@@ -85,6 +85,11 @@ struct DevNode {
     uint32_t gk_shift, cmap_shift;
     uint32_t n_ipc;        // node IP classes
     uint32_t n_pair;       // covered PAIR tables (0: the evaluations skip the PAIR steps)
+    // dst records (kNodeList words): rec0 = word offset of the first record in the cross array
+    // (the numbering list words use); lrec != 0: a copy of them ends the image, at word lrec
+    // (record word p of the cross numbering is image word p - rec0 + lrec); launches that do not
+    // stage that part of the image clear lrec and read the cross array
+    uint32_t rec0, lrec;
 };
 
 // Hit counters of a node table set with more slots than the LDS histogram holds (PERPOD / CONN
@@ -165,6 +170,7 @@ struct Tuning {
     uint32_t candi = 1;            // CANDI form (inline candidates) of dst-independent HBM-resident CAND tables
     uint32_t cross_max_rules = 1u << 20;  // CROSS (cross product) considered up to this many rules (within budget)
     uint32_t node_hist_cells = 4096;  // LDS hit-counter cells of a node set whose slots exceed the LDS histogram
+    uint32_t node_list_words = 4096;  // node dst records up to this many words go into the image (0 = never)
     // launches
     uint32_t blocks_per_cu = 0;    // cap on resident workgroups per CU (0 = occupancy)
     uint32_t stage_max_words = kStageBlobWords;  // table blobs staged whole in LDS

@@ -328,6 +328,9 @@ class Engine:
         base, common, pairs = C.c_uint64(), C.c_uint64(), C.c_uint64()
         self._ck(lib.pg_node_common_stats(self.h, C.byref(base), C.byref(common), C.byref(pairs)))
         st.update(base_image_bytes=base.value, common_row_pairs=common.value, table_ipclass_pairs=pairs.value)
+        rb, inimg = C.c_uint64(), C.c_int()
+        self._ck(lib.pg_node_list_stats(self.h, C.byref(rb), C.byref(inimg)))
+        st.update(list_record_bytes=rb.value, list_records_in_image=bool(inimg.value))
         return st
 
     def slot_of_rule(self, tid, idx):
