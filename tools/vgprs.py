@@ -22,7 +22,7 @@ for line in err.splitlines():
     if m and cur:
         rows[cur][m.group(1)] = int(m.group(2))
 for k, v in rows.items():
-    m = re.search(r"k_classifyILi(\d)ELb(\d)ELb(\d)ELi(\d)ELb(\d)ELi(\d+)E", k)
+    m = re.search(r"k_classifyILi(\d)ELb(\d)ELb(\d)ELi(\d+)ELb(\d)ELi(\d+)E", k)
     name = "classify<M%s C%s V%s S%s N%s %s>" % m.groups() if m else k[:40]
     print("%-32s vgpr %3d occ %2d scratch %d" % (name, v.get("VGPRs", -1), v.get("Occupancy [waves/SIMD]", -1),
                                                    v.get("ScratchSize [bytes/lane]", -1)))

@@ -239,7 +239,9 @@ PG_HD void probe_q(const DevTableSet& T, const uint32_t (&ip)[Q], End (&e)[Q]) {
 // kFullLds: lds (when set) holds every slot (node kernels); kAggGlobal: with lds unset, global
 // increments are aggregated per distinct slot over the wave (PERPOD node kernels)
 // kWin: node kernels, which may count through per-table windows (twin)
-template <bool kFullLds = false, bool kAggGlobal = false, bool kWin = false>
+// kFullOnly: node kernels whose LDS histogram holds every slot (device.hip STAGE + 16): an
+// increment is one LDS atomic, with none of the window / hot-slot / global tests in the code
+template <bool kFullLds = false, bool kAggGlobal = false, bool kWin = false, bool kFullOnly = false>
 struct HistT {
     uint32_t* lds;
     unsigned long long* glob;
@@ -295,6 +297,10 @@ struct HistT {
 #if defined(__HIP_DEVICE_COMPILE__) && defined(PG_PROBE_NOINC)  // measurement build only
         if (slot == 0xFFFFFFFFu) lds[0] = 0;
 #elif defined(__HIP_DEVICE_COMPILE__)
+        if constexpr (kFullOnly) {
+            atomicAdd(&lds[slot], 1u);
+            return;
+        }
         if (slot == hot) {
             nhot++;
             return;

@@ -424,6 +424,9 @@ __device__ __forceinline__ void stream_store(V v, V* p) {
 #ifndef PG_HOOK_LAST  // PF 2: the loads issued after the gathers of the group's last chunk (else its first)
 #define PG_HOOK_LAST 0
 #endif
+#ifndef PG_NODE_FULLH  // node kernels whose LDS histogram holds every slot: the specialised build (STAGE + 16)
+#define PG_NODE_FULLH 1
+#endif
 #ifndef PG_TPL  // tuples per lane per loop iteration (4 or 8)
 #define PG_TPL 4
 #endif
@@ -494,11 +497,13 @@ void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
                                                      uint32_t* __restrict__ out, unsigned long long* counters,
                                                      uint32_t stage_words, uint32_t hist_cells) {
     constexpr int STAGE = STAGE_ & 7;
-    constexpr bool NODST = MODE == 0 && STAGE_ >= 8;
+    constexpr bool NODST = MODE == 0 && (STAGE_ & 8);
+    // STAGE_ + 16 (node kernels with counters): the LDS histogram holds every slot (launcher)
+    constexpr bool FULLH = NODE && COUNT && (STAGE_ & 16);
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     uint32_t* hist = smem + (STAGE ? stage_words : 0u);
     // node kernels: the LDS histogram, when used, holds every slot (HistT<true>: no window test)
-    HistT<NODE, NODE && MODE == 1, NODE> h{nullptr, counters};
+    HistT<NODE, NODE && MODE == 1 && !FULLH, NODE && !FULLH, FULLH> h{nullptr, counters};
     DevTable tab0{};
     const uint32_t* blobs = T.blobs;
     // the node image: its LDS copy (at LDS address 0: LdsLoader) when staged, else global memory
@@ -532,7 +537,7 @@ void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
     // node kernels over more slots than the full histogram holds count through per-table
     // windows (device.hpp HistWindows; hist_cells + 2 = their cells) when the set has them, else
     // with global atomics only
-    const bool lds_hist = COUNT && (!NODE || hist_cells >= T.n_slots);
+    const bool lds_hist = FULLH || (COUNT && (!NODE || hist_cells >= T.n_slots));
     const bool twin = NODE && COUNT && !lds_hist && T.hist_cells != 0;
     const bool has_hist = COUNT && (!NODE || lds_hist || twin);  // an LDS histogram was allocated
     const uint32_t wn = COUNT ? hist_cells : 0u;
@@ -928,7 +933,7 @@ static void launch_one(const DevTableSet& T, const Tuning& tu, int t, const uint
                        const uint16_t* dport, const uint8_t* proto, uint64_t n, uint32_t* out,
                        unsigned long long* counters, hipStream_t st, size_t hist, uint32_t cells, uint32_t stage,
                        uint64_t items) {
-    if constexpr (STAGE) {
+    if constexpr ((STAGE & 7) != 0) {
         // 512 (A/B on MI355X: SINGLE with counters +14 % over 1024 at config 2; without
         // counters +2.5 % since SINGLE classifies one tuple per chunk, v15; config 4 over its
         // 12-bit staged root 163 vs 132 Gpps at 1024)
@@ -1016,20 +1021,29 @@ static void launch_classify(const DevTableSet& T, const Tuning& tu, int t, const
         auto fits = [&](uint32_t w) {
             return hist + (size_t)w * 4 <= tu.node_common_lds_max && w <= tu.node_stage_max_words + kCommonStageExtraWords;
         };
+        // (+ 16: counters in an LDS histogram of every slot, k_classify FULLH)
+        const bool full = PG_NODE_FULLH && COUNT && T.n_slots <= kLdsHistMax - 2u;
+        auto go = [&](auto stage, const DevTableSet& Ts, uint32_t words) {
+            constexpr int S = decltype(stage)::value;
+            if constexpr (COUNT) {
+                if (full)
+                    return launch_one<MODE, COUNT, VEC, S + 16, true>(Ts, tu, t, src, dst, sport, dport, proto, n, out,
+                                                                      counters, st, hist, cells, words, items);
+            }
+            launch_one<MODE, COUNT, VEC, S, true>(Ts, tu, t, src, dst, sport, dport, proto, n, out, counters, st, hist,
+                                                  cells, words, items);
+        };
         if (T.node.cmap && (fits(all) || fits(norec))) {
             const uint32_t w = fits(all) ? all : norec;
             if (w < all) Tn.node.lrec = 0;
-            launch_one<MODE, COUNT, VEC, 3, true>(Tn, tu, t, src, dst, sport, dport, proto, n, out, counters, st, hist,
-                                                  cells, w, items);
+            go(std::integral_constant<int, 3>{}, Tn, w);
         } else if (T.node.img_words_base <= tu.node_stage_max_words) {
             // (without a common-row section the records follow the base image directly)
             const bool recs = !T.node.cmap && T.node.lrec && all <= tu.node_stage_max_words;
             if (!recs) Tn.node.lrec = 0;
-            launch_one<MODE, COUNT, VEC, 1, true>(Tn, tu, t, src, dst, sport, dport, proto, n, out, counters, st, hist,
-                                                  cells, recs ? all : T.node.img_words_base, items);
+            go(std::integral_constant<int, 1>{}, Tn, recs ? all : T.node.img_words_base);
         } else {
-            launch_one<MODE, COUNT, VEC, 0, true>(T, tu, t, src, dst, sport, dport, proto, n, out, counters, st, hist,
-                                                  cells, 0, items);
+            go(std::integral_constant<int, 0>{}, T, 0u);
         }
     } else {
         launch_one<MODE, COUNT, VEC, 0, false>(T, tu, t, src, dst, sport, dport, proto, n, out, counters, st, hist,
