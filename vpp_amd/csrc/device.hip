@@ -466,6 +466,9 @@ __device__ __forceinline__ void st_words(const Words<NW>& v, uint32_t* p) {
 // workgroups per CU; 1024-thread workgroups, registers held to 64 (8 waves per SIMD) and no
 // stream prefetch (its 13 registers) put 32 waves per CU instead of 16 (A/B on MI355X,
 // gpurun_out/abocc: 89.1 -> 103.4 Gpps; the same 64-register cap on PERPOD spills and loses)
+#ifndef PG_CONN_WPE8_ALL  // CONN without counters too (A/B on MI355X, config 5 without counters: 136 -> 146 Gpps)
+#define PG_CONN_WPE8_ALL 1
+#endif
 #ifndef PG_CONN_COUNT_WPE
 #define PG_CONN_COUNT_WPE 8
 #endif
@@ -483,7 +486,7 @@ __device__ __forceinline__ void st_words(const Words<NW>& v, uint32_t* p) {
 template <int MODE, bool COUNT, bool NODE, int STAGE = 1>
 constexpr int kernel_wpe() {
     return !NODE ? (MODE == 0 && ((STAGE & 7) == 0 || (STAGE & 7) == 2) ? PG_SINGLE_HBM_WPE : 1)
-                 : (MODE == 2 && COUNT ? PG_CONN_COUNT_WPE : PG_NODE_WPE);
+                 : (MODE == 2 && (COUNT || PG_CONN_WPE8_ALL) ? PG_CONN_COUNT_WPE : PG_NODE_WPE);
 }
 // STAGE_ + 8 (SINGLE, STAGE 0-2): the table is dst-free (kFlagDstFree: no rule tests dst), so
 // the dst stream is not read
@@ -611,7 +614,7 @@ void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
     constexpr int PF0 = FD ? PG_PREFETCH_FD
                           : (PG_PREFETCH >= 0 ? PG_PREFETCH
                                               : ((MODE == 0 && STAGE != 0 && STAGE != 2) ||
-                                                 (NODE && MODE == 2 && COUNT && kernel_wpe<MODE, COUNT, NODE>() >= 8)
+                                                 (NODE && MODE == 2 && kernel_wpe<MODE, COUNT, NODE>() >= 8)
                                                      ? 0 : 1));
     constexpr int PF = (!NODE && PF0 == 2) ? 1 : PF0;  // (only node kernels have the gather hook)
     // PD = 2 (PG_PF_DEPTH): the loads run two groups ahead (group q + 2 * stride is
@@ -938,7 +941,7 @@ static void launch_one(const DevTableSet& T, const Tuning& tu, int t, const uint
         // counters +2.5 % since SINGLE classifies one tuple per chunk, v15; config 4 over its
         // 12-bit staged root 163 vs 132 Gpps at 1024)
         const uint32_t bs = tu.block_stage ? tu.block_stage
-                                           : (NODE && MODE == 2 && COUNT && kernel_wpe<MODE, COUNT, NODE>() >= 8 ? 1024u
+                                           : (NODE && MODE == 2 && kernel_wpe<MODE, COUNT, NODE>() >= 8 ? 1024u
                                                                                                                 : 512u);
         if (bs == 1024u)
             return launch_bs<MODE, COUNT, VEC, STAGE, NODE, 1024>(T, tu, t, src, dst, sport, dport, proto, n, out,
