@@ -151,7 +151,10 @@ int pg_ctx_device(const pg_ctx* ctx);
  * default 80 KiB), "block_stage" (workgroup size of LDS-staged classify launches: 256, 512 or
  * 1024; default 0 = per mode), "hist_window" (hit counters of a table set with more than 16382
  * slots: LDS cells kept for the classified table's first rules -- its default-deny slot and last
- * rule always get one -- the rest counted with global atomics; default 4096);
+ * rule always get one -- the rest counted with global atomics; default 4096), "node_hist_cells"
+ * (PERPOD / CONN launches over a table set with more than 16382 slots: cells of the LDS cache the
+ * hit counters go through -- the hottest slots of each workgroup's stream claim them, the rest
+ * take global atomics -- rounded down to a power of two, up to 8192; default 256, < 16 = none);
  * table compiler (the context recompiles and re-uploads on its next use; hit counters restart)
  * -- "root_bits_max" (cap of the src/key trie root stride, 4..16, default 16), "node_build"
  * (1/0: build the node classifier for PERPOD / CONN, default 1), "node_root_bits" (its IPv4 /

@@ -389,12 +389,12 @@ def test_large_table_root_staged_and_hbm_walks_equal_oracle():
 
 
 @pytest.mark.parametrize("mode", [MODE_PERPOD, MODE_CONN])
-def test_large_node_set_counter_windows_vs_oracle(mode):
+def test_large_node_set_counter_cache_vs_oracle(mode):
     """Config 6 (K8s objects -> 52 tables, 64.6k rules: more counter slots than the full LDS
-    histogram) with hit counters through the node classifier: per-table LDS windows
-    (node_hist_cells cells; a tiny budget; none = global atomics only) all give counters equal to
-    the oracle's histogram (PERPOD: of the verdict slots; CONN: of every evaluation), and the
-    verdicts stay bit-exact."""
+    histogram) with hit counters through the node classifier: the LDS slot cache (8192 / the
+    default 256 / 64 cells -- a tiny cache spills most slots to global atomics --; 0 = global
+    atomics only) gives counters equal to the oracle's histogram (PERPOD: of the verdict slots;
+    CONN: of every evaluation), and the verdicts stay bit-exact."""
     from oracle import world as OW
     from vpp_amd import workloads as W
     w = W.config6(0, n_tuples=1 << 20)
@@ -405,7 +405,7 @@ def test_large_node_set_counter_windows_vs_oracle(mode):
     torch.cuda.synchronize()
     tup = b.numpy(b.n)
     act, slot, hist = OW.expected(e, mode, -1, w.local_ifs, w.node_if, *tup, threads=16)
-    for cells in (4096, 300, 0):
+    for cells in (8192, 256, 64, 0):
         e.set_tuning("node_hist_cells", cells)
         out = torch.empty(b.n, dtype=torch.int32, device="cuda")
         cnt = torch.zeros(e.num_counter_slots(), dtype=torch.int64, device="cuda")

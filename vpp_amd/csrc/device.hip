@@ -159,8 +159,6 @@ DeviceBuffers* dev_upload(const HostTableSet& h, std::string* err) {
     size_t o_ip = place(h.iphash.size() * 4);
     size_t o_nimg = place(h.node_img.size() * 4);
     size_t o_nx = place(h.node_cross.size() * 4);
-    size_t o_tw = place(h.hist.tabwin.size() * 4);
-    size_t o_cs = place(h.hist.cell_slot.size() * 4);
     std::vector<uint8_t> img(off, 0);
     auto put = [&](size_t o, const void* p, size_t n) {
         if (n) std::memcpy(img.data() + o, p, n);
@@ -172,8 +170,6 @@ DeviceBuffers* dev_upload(const HostTableSet& h, std::string* err) {
     put(o_ip, h.iphash.data(), h.iphash.size() * 4);
     put(o_nimg, h.node_img.data(), h.node_img.size() * 4);
     put(o_nx, h.node_cross.data(), h.node_cross.size() * 4);
-    put(o_tw, h.hist.tabwin.data(), h.hist.tabwin.size() * 4);
-    put(o_cs, h.hist.cell_slot.data(), h.hist.cell_slot.size() * 4);
     auto* b = new DeviceBuffers();
     b->blob = dev_alloc(off, err);
     if (!b->blob) {
@@ -205,9 +201,6 @@ DeviceBuffers* dev_upload(const HostTableSet& h, std::string* err) {
     v.node = h.node;
     v.node.img = h.node_img.empty() ? nullptr : (const uint32_t*)(base + o_nimg);
     v.node.cross = h.node_img.empty() ? nullptr : (const uint32_t*)(base + o_nx);
-    v.hist_cells = (uint32_t)h.hist.cell_slot.size();
-    v.hist_tabwin = v.hist_cells ? (const uint32_t*)(base + o_tw) : nullptr;
-    v.hist_cell_slot = v.hist_cells ? (const uint32_t*)(base + o_cs) : nullptr;
     b->host_tabs = h.tabs;
     b->host_blob_words = h.blob_words;
     b->host_blob_prefix = h.blob_prefix;
@@ -537,19 +530,18 @@ void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
     // favours them: config 4's Zipf depth) and the extra cells its default-deny slot and its
     // last rule (a deny-the-rest / allow-all catch-all takes every unmatched packet: a single
     // global address would serialise them); node modes: "no ACL", "unresolved"
-    // node kernels over more slots than the full histogram holds count through per-table
-    // windows (device.hpp HistWindows; hist_cells + 2 = their cells) when the set has them, else
-    // with global atomics only
+    // node kernels over more slots than the full histogram holds count through an LDS slot
+    // cache of hist_cells (a power of two) cells (HistT kCache), else with global atomics only
     const bool lds_hist = FULLH || (COUNT && (!NODE || hist_cells >= T.n_slots));
-    const bool twin = NODE && COUNT && !lds_hist && T.hist_cells != 0;
-    const bool has_hist = COUNT && (!NODE || lds_hist || twin);  // an LDS histogram was allocated
+    const bool cache = NODE && COUNT && !lds_hist && hist_cells != 0;
+    const bool has_hist = COUNT && (!NODE || lds_hist || cache);  // an LDS histogram was allocated
     const uint32_t wn = COUNT ? hist_cells : 0u;
     const uint32_t wbase = (MODE == 0 && wn < T.n_slots) ? min(tab0.rule_base, T.n_slots - wn) : 0u;
     const uint32_t xslot = MODE == 0 ? (tab0.dflt & kSlotMask) : T.slot_noacl;
     const uint32_t xslot1 = MODE == 0 ? (tab0.n_rules ? tab0.rule_base + tab0.n_rules - 1u : xslot) : T.slot_unresolved;
     if (COUNT) {
-        if (has_hist)
-            for (uint32_t i = threadIdx.x; i <= wn + (twin ? 2u : 1u); i += BS) hist[i] = 0;
+        if (has_hist && !cache)
+            for (uint32_t i = threadIdx.x; i <= wn + 1u; i += BS) hist[i] = 0;
         h.lds = lds_hist ? hist : nullptr;
         h.wbase = wbase;
         h.wn = wn;
@@ -557,24 +549,22 @@ void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
         h.xslot1 = xslot1;
         h.full = wn >= T.n_slots;
         if (MODE == 0 && PG_HOT_SLOT) h.hot = xslot1;
-        // node kernels whose table set has more slots than the LDS histogram holds (every
-        // increment a global atomic): the catch-all of the node-output interface's outbound
-        // table (traffic to remote pods and the Internet) in a register -- config 6 with
-        // counters 0.4 -> 5.6 Gpps; with the histogram in LDS it costs 2 % (configs 3, 5)
+        // node kernels whose table set has more slots than the LDS histogram holds: the
+        // catch-all of the node-output interface's outbound table (traffic to remote pods and
+        // the Internet) in a register -- config 6 with counters 0.4 -> 5.6 Gpps when every
+        // increment was a global atomic; with the histogram in LDS it costs 2 % (configs 3, 5)
         if (MODE != 0 && PG_HOT_SLOT_NODE && !lds_hist && T.node_out >= 0) {
             const DevTable no = load_tab(T.tabs, T.node_out);
             if (no.n_rules) h.hot = no.rule_base + no.n_rules - 1u;
         }
-        if (twin) {  // the windows {rb, n, cb, h} per table, after the cells (16-B aligned)
-            uint4* tw = reinterpret_cast<uint4*>(hist + ((wn + 2u + 1u + 3u) & ~3u));
-            const uint4* g = reinterpret_cast<const uint4*>(T.hist_tabwin);
-            for (uint32_t i = threadIdx.x; i < T.n_tables; i += BS) tw[i] = g[i];
-            h.twin = reinterpret_cast<const uint32_t*>(tw);
-            h.wlds = hist;
-            h.nr = T.n_rules;
-            // the register-counted hot slot (the node-output table's catch-all) goes to the extra
-            // cell after the windows' cells at the flush
-            h.hotcell = wn + 2u;
+        if (cache) {  // keys [0, wn] then counts [0, wn]; cell wn holds the register-counted hot slot
+            for (uint32_t i = threadIdx.x; i <= wn; i += BS) {
+                hist[i] = i == wn ? h.hot : kCacheEmpty;
+                hist[wn + 1u + i] = 0u;
+            }
+            h.ckey = hist;
+            h.cmask = wn - 1u;
+            h.cshift = 32u - (uint32_t)__builtin_ctz(wn);
         }
     }
     if (STAGE || COUNT) __syncthreads();
@@ -701,10 +691,10 @@ void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
     if (COUNT) {
         h.flush_hot();
         __syncthreads();
-        for (uint32_t i = threadIdx.x; has_hist && i <= wn + (twin ? 2u : 1u); i += BS) {
-            const uint32_t v = hist[i];
-            const uint32_t slot = twin ? (i < wn + 2u ? T.hist_cell_slot[i] : h.hot)
-                                       : (i < wn ? wbase + i : (i == wn ? xslot : xslot1));
+        for (uint32_t i = threadIdx.x; has_hist && i <= wn + 1u; i += BS) {
+            if (cache && i > wn) break;
+            const uint32_t v = cache ? hist[wn + 1u + i] : hist[i];
+            const uint32_t slot = cache ? hist[i] : (i < wn ? wbase + i : (i == wn ? xslot : xslot1));
 #if !defined(PG_PROBE_NOFLUSH)  // measurement build only: the histogram is not flushed
             if (v) atomicAdd(&counters[slot], (unsigned long long)v);
 #endif
@@ -978,9 +968,8 @@ static void launch_classify(const DevTableSet& T, const Tuning& tu, int t, const
                             const uint16_t* sport, const uint16_t* dport, const uint8_t* proto, uint64_t n,
                             uint32_t* out, unsigned long long* counters, hipStream_t st) {
     // hit-counter LDS histogram (k_classify): every slot + 2 cells; or (more slots than fit) a
-    // SINGLE table's window of hist_window cells + 2; or the node set's per-table windows
-    // (HistWindows: their cells, one for the register-counted hot slot, then the windows
-    // themselves, 16 B per table); a node set without windows counts with global atomics only
+    // SINGLE table's window of hist_window cells + 2; or a node set's slot cache (node_hist_cells
+    // rounded down to a power of two; 0 = global atomics only)
     const bool node = MODE != 0 && tu.node_path && T.node.img;
     uint32_t cells = 0;
     size_t hist = 0;
@@ -991,9 +980,9 @@ static void launch_classify(const DevTableSet& T, const Tuning& tu, int t, const
         } else if (!node) {
             cells = std::min(tu.hist_window, kLdsHistMax - 2u);
             hist = ((size_t)cells + 2u) * 4;
-        } else if (T.hist_cells) {
-            cells = T.hist_cells - 2u;
-            hist = (((size_t)T.hist_cells + 1u + 3u) & ~(size_t)3) * 4 + (size_t)T.n_tables * 16;
+        } else if (tu.node_hist_cells >= 16u) {  // the slot cache: 2^k cells of {key, count} + the hot cell
+            cells = 1u << (31 - __builtin_clz(tu.node_hist_cells));
+            hist = ((size_t)cells + 1u) * 8;
         }
     }
     const uint64_t items = VEC ? (n + PG_TPL - 1) / PG_TPL : n;

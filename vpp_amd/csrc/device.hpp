@@ -92,17 +92,6 @@ struct DevNode {
     uint32_t rec0, lrec;
 };
 
-// Hit counters of a node table set with more slots than the LDS histogram holds (PERPOD / CONN
-// with counters): per-table windows of LDS cells. Cells [0, T + 2) count slots NR + c (the
-// tables' default slots, "no ACL", "unresolved"); table t's cells start at cb_t: its first h_t
-// rules, then its last rule (the catch-all every unmatched packet of a renderer table takes).
-// An evaluation's slot s of table t goes to cell cb_t + (s - rb_t) when s - rb_t < h_t, to
-// cb_t + h_t when s is the last rule, else to a global atomic; the flush maps cells back to
-// slots through cell_slot.
-struct HistWindows {
-    std::vector<uint32_t> tabwin;     // uint4 per table {rb_t, n_t, cb_t, h_t}
-    std::vector<uint32_t> cell_slot;  // slot of every cell
-};
 // table sets of up to this many counter slots are counted by a full LDS histogram (one cell per
 // slot, 64 KiB with the two extra cells of a SINGLE window)
 constexpr uint32_t kLdsHistCells = 16382;
@@ -123,10 +112,6 @@ struct DevTableSet {       // device pointers (valid on the GPU)
     uint32_t slot_unresolved;
     uint32_t n_slots;
     DevNode node;
-    // per-table hit-counter windows (HistWindows; hist_cells == 0: none)
-    const uint32_t* hist_tabwin;
-    const uint32_t* hist_cell_slot;
-    uint32_t hist_cells;
     const DevTable* host_tabs;       // host copies (launch decisions; not dereferenced on the GPU)
     const uint32_t* host_blob_words;
     const uint32_t* host_blob_prefix;  // FD blobs: words of the prefix a STAGE 5 launch stages
@@ -145,7 +130,6 @@ struct HostTableSet {
     int32_t node_if = -1, node_in = -1, node_out = -1;
     std::vector<uint32_t> node_img, node_cross;  // empty img: no node classifier
     DevNode node{};                              // header fields (pointers unset)
-    HistWindows hist;                            // empty: the node set's slots fit the LDS histogram
 };
 
 // table blobs up to this many words are staged in LDS by default (64 KiB); larger ones are
@@ -169,7 +153,8 @@ struct Tuning {
     uint32_t fd = 1;               // FD form of dst-independent CROSS tables that fit LDS
     uint32_t candi = 1;            // CANDI form (inline candidates) of dst-independent HBM-resident CAND tables
     uint32_t cross_max_rules = 1u << 20;  // CROSS (cross product) considered up to this many rules (within budget)
-    uint32_t node_hist_cells = 4096;  // LDS hit-counter cells of a node set whose slots exceed the LDS histogram
+    uint32_t node_hist_cells = 256;   // LDS slot-cache cells (rounded down to a power of two; < 16 = none)
+                                      // of node launches whose set has more slots than the LDS histogram
     uint32_t node_list_words = 4096;  // node dst records up to this many words go into the image (0 = never)
     // launches
     uint32_t blocks_per_cu = 0;    // cap on resident workgroups per CU (0 = occupancy)
@@ -213,8 +198,6 @@ struct NodePod {
 bool build_node(HostTableSet& h, const std::vector<TableAnalysis*>& an, const std::vector<NodePod>& pods,
                 const NodePod& node_end, const Tuning& tu);
 
-// engine.cpp: the per-table hit-counter windows of a node set (HistWindows) within `budget` cells
-void build_hist_windows(HostTableSet& h, uint32_t budget);
 
 struct GenParams {         // device view of pg_gen_spec
     uint64_t seed, index_base;

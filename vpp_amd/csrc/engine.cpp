@@ -54,7 +54,7 @@ const Knob kKnobs[] = {
     {"fd", &Tuning::fd, 0, 1, true},
     {"candi", &Tuning::candi, 0, 1, true},
     {"cross_max_rules", &Tuning::cross_max_rules, 0, 1 << 24, true},
-    {"node_hist_cells", &Tuning::node_hist_cells, 0, 16382, true},
+    {"node_hist_cells", &Tuning::node_hist_cells, 0, 8192, false},
     {"node_list_words", &Tuning::node_list_words, 0, 16384, true},
     {"blocks_per_cu", &Tuning::blocks_per_cu, 0, 64, false},
     {"stage_max_words", &Tuning::stage_max_words, 0, 36864, false},
@@ -394,41 +394,7 @@ void Engine::compile() {
     for (auto& e : ipmap) np.push_back(NodePod{e.ip, e.ifc, e.tin, e.tout});
     build_node(h, an, np, NodePod{0, h.node_if, h.node_in, h.node_out}, tune);
     for (TableAnalysis* a : an) free_analysis(a);
-    if (!h.node_img.empty() && NR + T + 2 > kLdsHistCells) build_hist_windows(h, tune.node_hist_cells);
     compiled = true;
-}
-
-// Per-table hit-counter windows of a node set too large for the full LDS histogram (device.hpp
-// HistWindows): within `budget` cells, T + 2 for the slots past the rules, one per table for
-// its last rule, and the largest uniform head window h (each table's first min(n_t - 1, h)
-// rules) that fits.
-void build_hist_windows(HostTableSet& h, uint32_t budget) {
-    const uint32_t T = (uint32_t)h.tabs.size(), NR = (uint32_t)h.rules.size();
-    h.hist = HistWindows();
-    uint64_t fixed = T + 2;
-    uint32_t maxn = 0;
-    for (const DevTable& d : h.tabs) fixed += d.n_rules ? 1 : 0, maxn = std::max(maxn, d.n_rules);
-    if (budget < fixed) return;
-    auto cells = [&](uint32_t w) {
-        uint64_t c = fixed;
-        for (const DevTable& d : h.tabs) c += d.n_rules ? std::min(d.n_rules - 1, w) : 0;
-        return c;
-    };
-    uint32_t lo = 0, hi = maxn;  // largest w with cells(w) <= budget
-    while (lo < hi) {
-        const uint32_t mid = lo + (hi - lo + 1) / 2;
-        if (cells(mid) <= budget) lo = mid;
-        else hi = mid - 1;
-    }
-    HistWindows& w = h.hist;
-    for (uint32_t c = 0; c < T + 2; c++) w.cell_slot.push_back(NR + c);
-    for (const DevTable& d : h.tabs) {
-        const uint32_t hd = d.n_rules ? std::min(d.n_rules - 1, lo) : 0;
-        const uint32_t cb = (uint32_t)w.cell_slot.size();
-        w.tabwin.insert(w.tabwin.end(), {d.rule_base, d.n_rules, cb, hd});
-        for (uint32_t i = 0; i < hd; i++) w.cell_slot.push_back(d.rule_base + i);
-        if (d.n_rules) w.cell_slot.push_back(d.rule_base + d.n_rules - 1);
-    }
 }
 
 }  // namespace pg
