@@ -23,7 +23,7 @@ for lib in $LIBS; do
         extra=""; case $c in r*) extra="--rules ${c#r}"; c=2;; esac
         step sweep $lib config $c $cnt $extra
         pre=""; for kv in ${PRE:-}; do pre="$pre --pre $kv"; done
-        VPP_AMD_LIB=$R/vpp_amd/$lib timeout -k 10 200 python tools/sweep.py --config ${c%c} --rounds 3 --reps 5 $cnt $pre \
+        VPP_AMD_LIB=$R/vpp_amd/$lib timeout -k 10 200 python tools/sweep.py --config ${c%c} --rounds 3 --reps 5 $cnt $pre $extra \
             >> "$O/sweep.jsonl" 2> "$O/sweep.err" || { tail -20 "$O/sweep.err"; exit 1; }
     done
 done
@@ -31,6 +31,6 @@ done
 python -c "
 import json
 for l in open('$O/sweep.jsonl'):
-    d=json.loads(l); print(d['lib'], d['config'], d['counters'], d['pre'], d['ms'], d['gpps'], d.get('out_sha'))
+    d=json.loads(l); print(d['lib'], d['config'], d.get('rules') or '', d['counters'], d['pre'], d['ms'], d['gpps'], d.get('out_sha'))
 "
 step done

@@ -295,7 +295,10 @@ PG_HD uint32_t fd_child(uint32_t e, uint32_t a) {
     return (e >> 10) + ((a >> (e & 31u)) & ((1u << w) - 1u));
 #endif
 }
-template <class LP, class LB, int Q>
+// SKIP (the src levels in HBM / L2): a lane whose src entry is already a self word (stride 0)
+// does not re-read it -- an exec-masked gather costs the texture path nothing for that lane, and
+// large FD tables are bound by that path (profiles/r03_v2_config7_util.json: TA busy 0.93)
+template <bool SKIP = false, class LP, class LB, int Q>
 PG_HD void fd_walk(const LP& lp, const LB& lb, uint32_t fsk, uint32_t kroot, uint32_t depth, uint32_t bias,
                    const uint32_t (&src)[Q], const uint32_t (&key)[Q], uint32_t (&w)[Q]) {
     const uint32_t ss = 32u - ((fsk >> 8) & 0xFFu), sk = 18u - ((fsk >> 16) & 0xFFu);
@@ -308,7 +311,7 @@ PG_HD void fd_walk(const LP& lp, const LB& lb, uint32_t fsk, uint32_t kroot, uin
     for (uint32_t l = 1; l < depth; l++) {
         PG_UNROLL
         for (int j = 0; j < Q; j++) {
-            es[j] = lb.u32(fd_child(es[j], src[j]));
+            if (!SKIP || (es[j] & 0x3E0u)) es[j] = lb.u32(fd_child(es[j], src[j]));
             ek[j] = lp.u32(fd_child(ek[j], key[j]));
         }
     }

@@ -579,7 +579,7 @@ int pg_debug_walk_stats(pg_ctx* ctx, int table_id, const pg_tuple_soa* t, uint64
                 const CountingLoader lp{blob, true, &nl, &nm};
                 const uint32_t s1[1] = {s}, k1[1] = {key};
                 uint32_t w1[1];
-                if (st == 5) fd_walk(lp, CountingLoader{blob, false, &nl, &nm}, hd.fsk, hd.kroot, hd.xoff, hd.nkc, s1, k1, w1);
+                if (st == 5) fd_walk<true>(lp, CountingLoader{blob, false, &nl, &nm}, hd.fsk, hd.kroot, hd.xoff, hd.nkc, s1, k1, w1);
                 else fd_walk(whole, whole, hd.fsk, hd.kroot, hd.xoff, hd.nkc, s1, k1, w1);
             } else {
                 const CountingLoader ld[1] = {whole};

@@ -13,6 +13,7 @@
 // flight (Q = 4 in the kernels' main loop, 1 in the remainder loop).
 #pragma once
 #include <cstdint>
+#include <type_traits>
 
 #include "blobwalk.hpp"
 #include "device.hpp"
@@ -26,6 +27,9 @@ namespace pg {
 #endif
 #ifndef PG_AGG_ROUNDS  // wave-aggregation rounds of hit-counter increments (Hist::inc)
 #define PG_AGG_ROUNDS 0
+#endif
+#ifndef PG_FD_SKIP  // FD walks over a blob in HBM: no re-read of a finished lane's self word
+#define PG_FD_SKIP 1
 #endif
 #ifndef PG_NODE_FB_Q1  // node kernels: per-table fallback one tuple at a time
 #define PG_NODE_FB_Q1 1
@@ -415,7 +419,8 @@ PG_HD void classify_fd_q(const DevTableSet& T, const LP& prefix, const LB& blob,
     bool any = false;
     PG_UNROLL
     for (int j = 0; j < Q; j++) key[j] = pkt_key(pr[j], dp[j]), any |= key[j] >= kWalkKeyLimit;
-    fd_walk(prefix, blob, tab0.fsk, tab0.kroot, tab0.xoff, tab0.nkc, s, key, out);
+    fd_walk<PG_FD_SKIP && !std::is_same<LB, LdsLoader>::value>(prefix, blob, tab0.fsk, tab0.kroot, tab0.xoff, tab0.nkc,
+                                                               s, key, out);
     if (any) {
         PG_UNROLL
         for (int j = 0; j < Q; j++)  // no rule of an FD table tests dst (engine.cpp): any dst will do

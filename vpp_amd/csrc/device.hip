@@ -405,8 +405,9 @@ __device__ __forceinline__ void stream_store(V v, V* p) {
 #ifndef PG_QSINGLE_FD  // SINGLE over an LDS-staged FD table (STAGE 4)
 #define PG_QSINGLE_FD 1
 #endif
-#ifndef PG_QSINGLE_FDG  // SINGLE over an FD table read from HBM, its prefix staged (STAGE 5)
-#define PG_QSINGLE_FDG 2
+#ifndef PG_QSINGLE_FDG  // SINGLE over an FD table read from HBM, its prefix staged (STAGE 5): 4 (A/B on
+                        // MI355X with the finished-lane skip: 30k / 100k / config 7 +2 / +1.2 / +1.2 % over 2)
+#define PG_QSINGLE_FDG 4
 #endif
 #ifndef PG_PREFETCH_FD  // STAGE 4 / 5: stream prefetch of the next group (see PG_PREFETCH)
 #define PG_PREFETCH_FD 0
