@@ -249,7 +249,9 @@ constexpr uint32_t kCacheEmpty = 0xFFFFFFFFu;  // slot-cache key of a free cell 
 #ifndef PG_CACHE_PROBES  // slot cache: cells tried (linear probing) before a global atomic
 #define PG_CACHE_PROBES 4
 #endif
-template <bool kFullLds = false, bool kAggGlobal = false, bool kCache = false, bool kFullOnly = false>
+// kHotRegs (kFullOnly builds): slots hot and hot2 are counted in registers
+template <bool kFullLds = false, bool kAggGlobal = false, bool kCache = false, bool kFullOnly = false,
+          bool kHotRegs = false>
 struct HistT {
     uint32_t* lds;
     unsigned long long* glob;
@@ -260,8 +262,8 @@ struct HistT {
     // SINGLE kernels: slot `hot` (the table's last rule: a catch-all takes every unmatched
     // packet) counted per lane in a register and added once at the end (flush_hot) -- many
     // lanes of a wave on one LDS address serialise their atomics
-    uint32_t hot = 0xFFFFFFFFu;
-    mutable uint32_t nhot = 0;
+    uint32_t hot = 0xFFFFFFFFu, hot2 = 0xFFFFFFFFu;  // (hot2: kFullOnly builds only)
+    mutable uint32_t nhot = 0, nhot2 = 0;
     // node kernels over a table set with more slots than the full histogram: an LDS cache of
     // 2^k cells, keys ckey[0, cmask] and counts after them (ckey[cmask + 2 + c]); cell cmask + 1
     // holds `hot`. A slot takes the first cell, from hash(slot) on, that holds it or that it
@@ -322,7 +324,12 @@ struct HistT {
 #if defined(__HIP_DEVICE_COMPILE__) && defined(PG_PROBE_NOINC)  // measurement build only
         if (slot == 0xFFFFFFFFu) lds[0] = 0;
 #elif defined(__HIP_DEVICE_COMPILE__)
-        if constexpr (kFullOnly) {
+        if constexpr (kFullOnly && kHotRegs) {  // CONN's two hottest slots in registers
+            nhot += slot == hot;
+            nhot2 += slot == hot2;
+            if (slot != hot && slot != hot2) atomicAdd(&lds[slot], 1u);
+            return;
+        } else if constexpr (kFullOnly) {
             atomicAdd(&lds[slot], 1u);
             return;
         }
@@ -390,6 +397,10 @@ struct HistT {
     }
     PG_HD void flush_hot() const {  // device: the register count of `hot` into the histogram
 #if defined(__HIP_DEVICE_COMPILE__)
+        if (kHotRegs && nhot2) {
+            atomicAdd(&lds[hot2], nhot2);
+            nhot2 = 0;
+        }
         if (nhot) {
             const uint32_t h0 = hot;
             const uint32_t n = nhot;
@@ -872,7 +883,18 @@ PG_HD void classify_node_q(const DevTableSet& T, const DevNode& N, const L& img,
         uint32_t keys[Q];
         PG_UNROLL
         for (int j = 0; j < Q; j++) keys[j] = key[j] < kWalkKeyLimit ? key[j] : 0u;
+#if defined(PG_PROBE_NODSTWALK)  // measurement build only: PERPOD walks src only (dst class = src's)
+        {
+            uint32_t sa[Q], sc[Q];
+            PG_UNROLL
+            for (int j = 0; j < Q; j++) sa[j] = ips[j];
+            node_trie2_q<PRED>(img, N, sa, sc, keys, gs);
+            PG_UNROLL
+            for (int j = 0; j < Q; j++) ipc[j] = sc[j], ipc[Q + j] = sc[j];
+        }
+#else
         node_trie2_q<PRED>(img, N, ips, ipc, keys, gs);
+#endif
         PG_UNROLL
         for (int j = 0; j < Q; j++) ga[j] = gs[j];
     }

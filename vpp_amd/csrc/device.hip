@@ -198,6 +198,15 @@ DeviceBuffers* dev_upload(const HostTableSet& h, std::string* err) {
     v.slot_noacl = v.n_rules + v.n_tables;
     v.slot_unresolved = v.slot_noacl + 1;
     v.n_slots = v.slot_unresolved + 1;
+    {
+        std::vector<uint32_t> uses(h.tabs.size(), 0);
+        for (size_t i = 0; i + 1 < h.ifaces.size(); i += 2)
+            if (h.ifaces[i] >= 0 && (size_t)h.ifaces[i] < uses.size()) uses[h.ifaces[i]]++;
+        v.slot_hot_in = 0xFFFFFFFFu;
+        uint32_t best = 1;  // shared by two interfaces at least
+        for (size_t t = 0; t < uses.size(); t++)
+            if (uses[t] > best && h.tabs[t].n_rules) best = uses[t], v.slot_hot_in = h.tabs[t].rule_base + h.tabs[t].n_rules - 1u;
+    }
     v.node = h.node;
     v.node.img = h.node_img.empty() ? nullptr : (const uint32_t*)(base + o_nimg);
     v.node.cross = h.node_img.empty() ? nullptr : (const uint32_t*)(base + o_nx);
@@ -418,6 +427,9 @@ __device__ __forceinline__ void stream_store(V v, V* p) {
 #ifndef PG_HOOK_LAST  // PF 2: the loads issued after the gathers of the group's last chunk (else its first)
 #define PG_HOOK_LAST 0
 #endif
+#ifndef PG_CONN_HOT_REGS  // CONN full-histogram build: two hot slots counted in registers
+#define PG_CONN_HOT_REGS 1
+#endif
 #ifndef PG_NODE_FULLH  // node kernels whose LDS histogram holds every slot: the specialised build (STAGE + 16)
 #define PG_NODE_FULLH 1
 #endif
@@ -500,7 +512,8 @@ void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     uint32_t* hist = smem + (STAGE ? stage_words : 0u);
     // node kernels: the LDS histogram, when used, holds every slot (HistT<true>: no window test)
-    HistT<NODE, NODE && MODE == 1 && !FULLH, NODE && !FULLH, FULLH> h{nullptr, counters};
+    HistT<NODE, NODE && MODE == 1 && !FULLH, NODE && !FULLH, FULLH, FULLH && MODE == 2 && PG_CONN_HOT_REGS> h{nullptr,
+                                                                                                  counters};
     DevTable tab0{};
     const uint32_t* blobs = T.blobs;
     // the node image: its LDS copy (at LDS address 0: LdsLoader) when staged, else global memory
@@ -550,6 +563,10 @@ void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
         h.xslot1 = xslot1;
         h.full = wn >= T.n_slots;
         if (MODE == 0 && PG_HOT_SLOT) h.hot = xslot1;
+        if (FULLH && MODE == 2 && PG_CONN_HOT_REGS) {  // "no ACL" and the most shared inbound ACL's last rule
+            h.hot = T.slot_noacl;
+            h.hot2 = T.slot_hot_in;
+        }
         // node kernels whose table set has more slots than the LDS histogram holds: the
         // catch-all of the node-output interface's outbound table (traffic to remote pods and
         // the Internet) in a register -- config 6 with counters 0.4 -> 5.6 Gpps when every

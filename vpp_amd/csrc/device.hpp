@@ -111,6 +111,10 @@ struct DevTableSet {       // device pointers (valid on the GPU)
     uint32_t slot_noacl;   // NR + T
     uint32_t slot_unresolved;
     uint32_t n_slots;
+    // the last rule of the inbound ACL the most interfaces share (the renderer's reflective ACL
+    // for the pods without an ingress policy), 0xFFFFFFFF = none: CONN kernels count it, like "no
+    // ACL", in a register
+    uint32_t slot_hot_in;
     DevNode node;
     const DevTable* host_tabs;       // host copies (launch decisions; not dereferenced on the GPU)
     const uint32_t* host_blob_words;
