@@ -107,64 +107,103 @@ PG_HD bool rec_match(const W4& r, uint32_t dst, uint32_t key) {
 // wasted read costs little and per-lane branches cost exec-mask juggling.
 // ld0: loaders for the src trie root (a blob whose root alone is staged in LDS: ld0 reads the
 // LDS copy, ld the blob in HBM; otherwise the same loaders).
+// CANDI lanes (ci) of a walk: the 4-B root (ld0), then 8-B entries until an inline candidate
+// (w set) or a pointer to the class's record list (pend, pos: the caller walks the records,
+// rec_walk). A lane that finished issues no further load.
+template <class L, class L0, int Q>
+PG_HD void candi_walk(const L (&ld)[Q], const L0 (&ld0)[Q], const BlobTab (&tb)[Q], const bool (&ci)[Q],
+                      const uint32_t (&src)[Q], const uint32_t (&key)[Q], uint32_t (&w)[Q], bool (&pend)[Q],
+                      uint32_t (&pos)[Q]) {
+    uint32_t cw[Q], cst[Q], ss[Q];
+    bool cwalk[Q];
+    PG_UNROLL
+    for (int j = 0; j < Q; j++) {
+        cwalk[j] = false;
+        cw[j] = cst[j] = ss[j] = 0;
+        if (!ci[j]) continue;
+        ss[j] = 32u - ((tb[j].fsk >> 8) & 0xFFu);
+        const uint32_t e = ld0[j].u32(kSrcRoot + (src[j] >> ss[j]));
+        if (e & kLeaf) {
+            pos[j] = tb[j].xoff + 4u * (e & ~kLeaf);
+            pend[j] = true;
+        } else {
+            cw[j] = trie_child(e);
+            cst[j] = trie_stride(e);
+            cwalk[j] = true;
+        }
+    }
+    for (;;) {
+        bool more = false;
+        PG_UNROLL
+        for (int j = 0; j < Q; j++) more |= cwalk[j];
+        if (!more) break;
+        PG_UNROLL
+        for (int j = 0; j < Q; j++) {
+            if (!cwalk[j]) continue;
+            ss[j] -= cst[j];
+            const W2 v = ld[j].u2(cw[j] + 2u * ((src[j] >> ss[j]) & ((1u << cst[j]) - 1u)));
+            if (v.y & kCandiNode) {
+                if (v.y & kCandiInternal) {
+                    cw[j] = v.x;
+                    cst[j] = v.y & 31u;
+                } else {
+                    pos[j] = tb[j].xoff + 4u * v.x;
+                    pend[j] = true;
+                    cwalk[j] = false;
+                }
+            } else {
+                const uint32_t klo = v.x & 0x3FFFFu, khi = (v.x >> 18) | ((v.y & 15u) << 14);
+                const uint32_t rel = (v.y >> 6) & kCandiDefault;
+                const bool hit = key[j] >= klo && key[j] <= khi && rel != kCandiDefault;
+                w[j] = hit ? (((v.y >> 4) & 3u) << 30) | (tb[j].rbase + rel) : tb[j].dflt;
+                cwalk[j] = false;
+            }
+        }
+    }
+}
+
+// records of the pend lanes until the first match (every list ends with a match-all record or
+// flags its last one: no match there -> the table's default)
+template <class L, int Q>
+PG_HD void rec_walk(const L (&ld)[Q], const BlobTab (&tb)[Q], const uint32_t (&dst)[Q], const uint32_t (&key)[Q],
+                    bool (&pend)[Q], uint32_t (&pos)[Q], uint32_t (&w)[Q]) {
+    for (;;) {
+        bool more = false;
+        PG_UNROLL
+        for (int j = 0; j < Q; j++) more |= pend[j];
+        if (!more) break;
+        PG_UNROLL
+        for (int j = 0; j < Q; j++) {
+            if (!pend[j]) continue;
+            const W4 r = ld[j].u4(pos[j]);
+            if (rec_match(r, dst[j], key[j])) {
+                w[j] = r.w;
+                pend[j] = false;
+            } else if (r.y & kRecLast) {
+                w[j] = tb[j].dflt;
+                pend[j] = false;
+            } else {
+                pos[j] += 4u;
+            }
+        }
+    }
+}
+
 template <bool PRED = false, class L, class L0, int Q>
 PG_HD void blob_walk(const L (&ld)[Q], const L0 (&ld0)[Q], const BlobTab (&tb)[Q], const bool (&on)[Q],
                      const uint32_t (&src)[Q], const uint32_t (&dst)[Q], const uint32_t (&key)[Q], uint32_t (&w)[Q]) {
     uint32_t es[Q], ek[Q], ss[Q], sk[Q], ed[Q], sd[Q];
-    // CANDI lanes (blobwalk.hpp kFlagCandI): 8-B entries below the root, inline candidates
-    uint32_t cw[Q], cst[Q], pos[Q];
-    bool ci[Q], cwalk[Q], pend[Q], anyci = false;
+    // CANDI lanes (kFlagCandI): 8-B entries below the root, inline candidates (candi_walk)
+    uint32_t pos[Q];
+    bool ci[Q], pend[Q], anyci = false;
     PG_UNROLL
     for (int j = 0; j < Q; j++) {
         ci[j] = on[j] && (tb[j].fsk & kFlagCandI);
         anyci |= ci[j];
-        cwalk[j] = pend[j] = false;
-        pos[j] = cw[j] = cst[j] = 0;
+        pend[j] = false;
+        pos[j] = 0;
     }
-    if (anyci) {
-        PG_UNROLL
-        for (int j = 0; j < Q; j++) {
-            if (!ci[j]) continue;
-            ss[j] = 32u - ((tb[j].fsk >> 8) & 0xFFu);
-            const uint32_t e = ld0[j].u32(kSrcRoot + (src[j] >> ss[j]));
-            if (e & kLeaf) {
-                pos[j] = tb[j].xoff + 4u * (e & ~kLeaf);
-                pend[j] = true;
-            } else {
-                cw[j] = trie_child(e);
-                cst[j] = trie_stride(e);
-                cwalk[j] = true;
-            }
-        }
-        for (;;) {
-            bool more = false;
-            PG_UNROLL
-            for (int j = 0; j < Q; j++) more |= cwalk[j];
-            if (!more) break;
-            PG_UNROLL
-            for (int j = 0; j < Q; j++) {
-                if (!cwalk[j]) continue;
-                ss[j] -= cst[j];
-                const W2 v = ld[j].u2(cw[j] + 2u * ((src[j] >> ss[j]) & ((1u << cst[j]) - 1u)));
-                if (v.y & kCandiNode) {
-                    if (v.y & kCandiInternal) {
-                        cw[j] = v.x;
-                        cst[j] = v.y & 31u;
-                    } else {
-                        pos[j] = tb[j].xoff + 4u * v.x;
-                        pend[j] = true;
-                        cwalk[j] = false;
-                    }
-                } else {
-                    const uint32_t klo = v.x & 0x3FFFFu, khi = (v.x >> 18) | ((v.y & 15u) << 14);
-                    const uint32_t rel = (v.y >> 6) & kCandiDefault;
-                    const bool hit = key[j] >= klo && key[j] <= khi && rel != kCandiDefault;
-                    w[j] = hit ? (((v.y >> 4) & 3u) << 30) | (tb[j].rbase + rel) : tb[j].dflt;
-                    cwalk[j] = false;
-                }
-            }
-        }
-    }
+    if (anyci) candi_walk(ld, ld0, tb, ci, src, key, w, pend, pos);
     PG_UNROLL
     for (int j = 0; j < Q; j++) {
         es[j] = ek[j] = ed[j] = kLeaf;
@@ -250,26 +289,7 @@ PG_HD void blob_walk(const L (&ld)[Q], const L0 (&ld0)[Q], const BlobTab (&tb)[Q
         }
     }
     // records until the first match (every list ends with a match-all record)
-    for (;;) {
-        bool more = false;
-        PG_UNROLL
-        for (int j = 0; j < Q; j++) more |= pend[j];
-        if (!more) break;
-        PG_UNROLL
-        for (int j = 0; j < Q; j++) {
-            if (!pend[j]) continue;
-            const W4 r = ld[j].u4(pos[j]);
-            if (rec_match(r, dst[j], key[j])) {
-                w[j] = r.w;
-                pend[j] = false;
-            } else if (r.y & kRecLast) {
-                w[j] = tb[j].dflt;
-                pend[j] = false;
-            } else {
-                pos[j] += 4u;
-            }
-        }
-    }
+    rec_walk(ld, tb, dst, key, pend, pos, w);
 }
 
 template <bool PRED = false, class L, int Q>

@@ -444,6 +444,45 @@ PG_HD void classify_fd_q(const DevTableSet& T, const LP& prefix, const LB& blob,
     }
 }
 
+// SINGLE mode over a CANDI table whose root alone is staged (uniform: tab0; device.hip STAGE 6):
+// the root from `root`, the 8-B entries and records from `blob`, with none of the generic blob
+// walk's per-lane structure tests; ANY-protocol packets take the linear scan. No rule of a CANDI
+// table tests dst (fastpath.cpp), so dst is not an input.
+template <bool COUNT, int Q, class L0, class L>
+PG_HD void classify_candi_q(const DevTableSet& T, const L0& root, const L& blob, const DevTable& tab0,
+                            const uint32_t (&s)[Q], const uint32_t (&dp)[Q], const uint32_t (&pr)[Q], const Hist& h,
+                            uint32_t (&out)[Q]) {
+    uint32_t key[Q], zero[Q], pos[Q];
+    bool on[Q], pend[Q], any = false;
+    L ld[Q];
+    L0 ld0[Q];
+    BlobTab tb[Q];
+    PG_UNROLL
+    for (int j = 0; j < Q; j++) {
+        key[j] = pkt_key(pr[j], dp[j]);
+        any |= key[j] >= kWalkKeyLimit;
+        zero[j] = 0;
+        pos[j] = 0;
+        on[j] = true;
+        pend[j] = false;
+        ld[j] = blob;
+        ld0[j] = root;
+        tb[j] = BlobTab{tab0.fsk, tab0.dflt, tab0.kroot, tab0.xoff, tab0.nkc, tab0.rule_base};
+    }
+    candi_walk(ld, ld0, tb, on, s, key, out, pend, pos);
+    rec_walk(ld, tb, zero, key, pend, pos, out);
+    if (any) {
+        PG_UNROLL
+        for (int j = 0; j < Q; j++)
+            if (key[j] >= kWalkKeyLimit)
+                out[j] = eval_linear(T.rules, tab0.rule_base, tab0.n_rules, tab0.dflt, s[j], 0u, key[j]);
+    }
+    if (COUNT) {
+        PG_UNROLL
+        for (int j = 0; j < Q; j++) h.inc(out[j] & kSlotMask);
+    }
+}
+
 // ---- evaluators: evalACL of Q tuples on tables t[j], forward (src -> dst, SYN key) or
 // reverse (dst -> src, SYN-ACK key; testConnection's second half) ----------------------------
 

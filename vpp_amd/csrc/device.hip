@@ -396,6 +396,9 @@ __device__ __forceinline__ void stream_store(V v, V* p) {
 // SINGLE: blob staged in LDS (STAGE 1) one tuple at a time (A/B on MI355X: config 2 331 / 343 /
 // 348 Gpps at 4 / 2 / 1, with counters 307 / 316 / 325), blob in HBM four (config 4 with the
 // inline-candidate form and a 12-bit staged root: 169.3 / 163.5 / 124 at 4 / 2 / 1)
+#ifndef PG_CANDI_LEAN  // SINGLE over a CANDI table with its root staged: the dedicated walk (STAGE 6)
+#define PG_CANDI_LEAN 1
+#endif
 #ifndef PG_QSINGLE_LDS
 #define PG_QSINGLE_LDS 1
 #endif
@@ -535,8 +538,8 @@ void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
             }
         }
     }
-    // STAGE 2: only the header and src-trie root of a large blob are in LDS
-    const uint32_t* rootb = (MODE == 0 && STAGE == 2) ? smem : nullptr;
+    // STAGE 2 / 6: only the header and src-trie root of a large blob are in LDS
+    const uint32_t* rootb = (MODE == 0 && (STAGE == 2 || STAGE == 6)) ? smem : nullptr;
     // hit counters: an LDS histogram of the window [wbase, wbase + wn) of slots plus cells for
     // slots xslot and xslot1, flushed with one u64 atomic per non-zero cell; slots outside go to
     // global atomics. Every slot fits the window unless the table set has more than
@@ -621,7 +624,7 @@ void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
     // four tuples per chunk: 172.9 vs 169.3 Gpps)
     constexpr int PF0 = FD ? PG_PREFETCH_FD
                           : (PG_PREFETCH >= 0 ? PG_PREFETCH
-                                              : ((MODE == 0 && STAGE != 0 && STAGE != 2) ||
+                                              : ((MODE == 0 && STAGE != 0 && STAGE != 2 && STAGE != 6) ||
                                                  (NODE && MODE == 2 && kernel_wpe<MODE, COUNT, NODE>() >= 8)
                                                      ? 0 : 1));
     constexpr int PF = (!NODE && PF0 == 2) ? 1 : PF0;  // (only node kernels have the gather hook)
@@ -675,6 +678,8 @@ void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
             if constexpr (FD) {
                 if constexpr (STAGE == 4) classify_fd_q<COUNT, QC>(T, LdsLoader{}, LdsLoader{}, tab0, cs, cdp, cpr, h, co);
                 else classify_fd_q<COUNT, QC>(T, LdsLoader{}, DevLoader{fd_blob}, tab0, cs, cdp, cpr, h, co);
+            } else if constexpr (MODE == 0 && STAGE == 6) {
+                classify_candi_q<COUNT, QC>(T, LdsLoader{}, DevLoader{T.blobs + tab0.blob_off}, tab0, cs, cdp, cpr, h, co);
             } else if constexpr (NODE) {
                 if (c == (PG_HOOK_LAST ? P - QC : 0))
                     classify_node_q<MODE, COUNT, QC, STAGE && PG_PRED, STAGE == 3>(T, T.node, img, cs, cd, csp, cdp, cpr, h, co, hook);
@@ -702,6 +707,8 @@ void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
         uint32_t o[1];
         if constexpr (FD && STAGE == 4) classify_fd_q<COUNT, 1>(T, LdsLoader{}, LdsLoader{}, tab0, s1, dp1, pr1, h, o);
         else if constexpr (FD) classify_fd_q<COUNT, 1>(T, LdsLoader{}, DevLoader{fd_blob}, tab0, s1, dp1, pr1, h, o);
+        else if constexpr (MODE == 0 && STAGE == 6)
+            classify_candi_q<COUNT, 1>(T, LdsLoader{}, DevLoader{T.blobs + tab0.blob_off}, tab0, s1, dp1, pr1, h, o);
         else if constexpr (NODE) classify_node_q<MODE, COUNT, 1, STAGE && PG_PRED, STAGE == 3>(T, T.node, img, s1, d1, sp1, dp1, pr1, h, o);
         else classify_q<MODE, COUNT, 1, STAGE == 1 && PG_PRED>(T, blobs, tab0, s1, d1, sp1, dp1, pr1, h, o, rootb);
         out[i] = o[0];
@@ -973,6 +980,9 @@ static void launch_generic(const DevTableSet& T, const Tuning& tu, int t, const 
     if (!(hd.fsk & kFlagLinear) && words && words <= tu.stage_max_words)
         launch_one<MODE, COUNT, VEC, 1 + NODST, false>(T, tu, t, src, dst, sport, dport, proto, n, out, counters, st,
                                                        hist, cells, words, items);
+    else if ((hd.fsk & kFlagCandI) && NODST && PG_CANDI_LEAN && root_words <= tu.stage_root_max_words)
+        launch_one<MODE, COUNT, VEC, 6 + NODST, false>(T, tu, t, src, dst, sport, dport, proto, n, out, counters, st,
+                                                       hist, cells, root_words, items);
     else if (!(hd.fsk & kFlagLinear) && words && root_words <= tu.stage_root_max_words)
         launch_one<MODE, COUNT, VEC, 2 + NODST, false>(T, tu, t, src, dst, sport, dport, proto, n, out, counters, st,
                                                        hist, cells, root_words, items);
