@@ -396,6 +396,13 @@ __device__ __forceinline__ void stream_store(V v, V* p) {
 // SINGLE: blob staged in LDS (STAGE 1) one tuple at a time (A/B on MI355X: config 2 331 / 343 /
 // 348 Gpps at 4 / 2 / 1, with counters 307 / 316 / 325), blob in HBM four (config 4 with the
 // inline-candidate form and a 12-bit staged root: 169.3 / 163.5 / 124 at 4 / 2 / 1)
+#ifndef PG_QCANDI  // STAGE 6 without counters (A/B on MI355X, config 4: 188.5 vs 179.5 Gpps at 4; with
+#define PG_QCANDI 2  // counters 4 stays: 113.5 vs 112)
+#endif
+#ifndef PG_FD_BS1024  // LDS-staged FD blobs that leave room for < 3 workgroups per CU: 1024 threads
+#define PG_FD_BS1024 1
+#endif
+constexpr size_t kLdsPerCU = 160u << 10;
 #ifndef PG_CANDI_LEAN  // SINGLE over a CANDI table with its root staged: the dedicated walk (STAGE 6)
 #define PG_CANDI_LEAN 1
 #endif
@@ -668,7 +675,9 @@ void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
         constexpr int QC = MODE == 2 ? (COUNT ? PG_QCONN_COUNT : PG_QCONN)
                                      : (MODE == 1 ? PG_QPOD
                                                   : (FD ? (STAGE == 4 ? PG_QSINGLE_FD : PG_QSINGLE_FDG)
-                                                                : (STAGE == 1 ? PG_QSINGLE_LDS : PG_QSINGLE)));
+                                                        : (STAGE == 1   ? PG_QSINGLE_LDS
+                                                           : STAGE == 6 ? (COUNT ? PG_QSINGLE : PG_QCANDI)
+                                                                        : PG_QSINGLE)));
 #pragma unroll
         for (int c = 0; c < P; c += QC) {
             uint32_t cs[QC], cd[QC], csp[QC], cdp[QC], cpr[QC], co[QC];
@@ -955,9 +964,15 @@ static void launch_one(const DevTableSet& T, const Tuning& tu, int t, const uint
         // 512 (A/B on MI355X: SINGLE with counters +14 % over 1024 at config 2; without
         // counters +2.5 % since SINGLE classifies one tuple per chunk, v15; config 4 over its
         // 12-bit staged root 163 vs 132 Gpps at 1024)
+        // 1024 for CONN (32 waves per CU at 64 registers) and for SINGLE over an LDS-staged FD
+        // blob whose LDS (+ histogram) leaves room for fewer than three workgroups per CU: one
+        // image copy then serves 16 waves (A/B on MI355X, the 10k-rule sweep table, 59.5 KB:
+        // 393.8 -> 471.5 Gpps; config 2's 49 KB blob, three fit: 530 vs 475 at 1024)
+        const size_t lds_bytes = hist + (size_t)stage * 4;
         const uint32_t bs = tu.block_stage ? tu.block_stage
-                                           : (NODE && MODE == 2 && kernel_wpe<MODE, COUNT, NODE>() >= 8 ? 1024u
-                                                                                                                : 512u);
+                            : (NODE && MODE == 2 && kernel_wpe<MODE, COUNT, NODE>() >= 8)           ? 1024u
+                            : (MODE == 0 && (STAGE & 7) == 4 && lds_bytes > kLdsPerCU / 3 && PG_FD_BS1024) ? 1024u
+                                                                                                     : 512u;
         if (bs == 1024u)
             return launch_bs<MODE, COUNT, VEC, STAGE, NODE, 1024>(T, tu, t, src, dst, sport, dport, proto, n, out,
                                                                   counters, st, hist, cells, stage, items);
