@@ -4,6 +4,7 @@
 # Configs: 3, 5c (with counters), r10000 (config 2 at 10k rules), ...
 #   gpurun -- bash tools/ab.sh TAG "libA libB" "3 5c 6" [pytest paths]
 # PRE="key=v ..." (environment): compiler knobs set before the tables are built (sweep.py --pre)
+# TUNE="key=v1,v2 ..." (environment): launch knobs swept inside each run (sweep.py --tune)
 set -o pipefail
 TAG=${1:-ablib}; LIBS=${2:-libpolicygpu.so}; CONFIGS=${3:-3}; TESTS=${4:-}
 R=$(pwd)
@@ -23,6 +24,7 @@ for lib in $LIBS; do
         extra=""; case $c in r*) extra="--rules ${c#r}"; c=2;; esac
         step sweep $lib config $c $cnt $extra
         pre=""; for kv in ${PRE:-}; do pre="$pre --pre $kv"; done
+        for kv in ${TUNE:-}; do pre="$pre --tune $kv"; done
         VPP_AMD_LIB=$R/vpp_amd/$lib timeout -k 10 200 python tools/sweep.py --config ${c%c} --rounds 3 --reps 5 $cnt $pre $extra \
             >> "$O/sweep.jsonl" 2> "$O/sweep.err" || { tail -20 "$O/sweep.err"; exit 1; }
     done
@@ -31,6 +33,9 @@ done
 python -c "
 import json
 for l in open('$O/sweep.jsonl'):
-    d=json.loads(l); print(d['lib'], d['config'], d.get('rules') or '', d['counters'], d['pre'], d['ms'], d['gpps'], d.get('out_sha'))
+    d = json.loads(l)
+    t={k: v for k, v in d.items() if k not in ('lib', 'config', 'rules', 'counters', 'pre', 'ns', 'ms', 'gpps', 'GBps',
+                                           'same_output', 'out_sha', 'blob')}
+    print(d['lib'], d['config'], d.get('rules') or '', d['counters'], d['pre'], t or '', d['ms'], d['gpps'], d.get('out_sha'))
 "
 step done

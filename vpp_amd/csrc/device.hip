@@ -482,6 +482,9 @@ __device__ __forceinline__ void st_words(const Words<NW>& v, uint32_t* p) {
 // workgroups per CU; 1024-thread workgroups, registers held to 64 (8 waves per SIMD) and no
 // stream prefetch (its 13 registers) put 32 waves per CU instead of 16 (A/B on MI355X,
 // gpurun_out/abocc: 89.1 -> 103.4 Gpps; the same 64-register cap on PERPOD spills and loses)
+#ifndef PG_POD_FULLH_WPE8  // PERPOD full-histogram build at 64 registers / 1024 threads / no prefetch
+#define PG_POD_FULLH_WPE8 1
+#endif
 #ifndef PG_CONN_WPE8_ALL  // CONN without counters too (A/B on MI355X, config 5 without counters: 136 -> 146 Gpps)
 #define PG_CONN_WPE8_ALL 1
 #endif
@@ -502,7 +505,17 @@ __device__ __forceinline__ void st_words(const Words<NW>& v, uint32_t* p) {
 template <int MODE, bool COUNT, bool NODE, int STAGE = 1>
 constexpr int kernel_wpe() {
     return !NODE ? (MODE == 0 && ((STAGE & 7) == 0 || (STAGE & 7) == 2) ? PG_SINGLE_HBM_WPE : 1)
-                 : (MODE == 2 && (COUNT || PG_CONN_WPE8_ALL) ? PG_CONN_COUNT_WPE : PG_NODE_WPE);
+                 : ((MODE == 2 && (COUNT || PG_CONN_WPE8_ALL)) || (MODE == 1 && COUNT && (STAGE & 16) && PG_POD_FULLH_WPE8)
+                        ? PG_CONN_COUNT_WPE : PG_NODE_WPE);
+}
+// node builds at 64 registers (wpe 8): 1024-thread workgroups and no stream prefetch (its
+// registers): CONN, and PERPOD counting into an LDS histogram of every slot (image + histogram
+// leave LDS for two workgroups per CU: 16 waves at 512 threads, 32 at 1024; A/B on MI355X,
+// config 3 with counters 227 -> 260 Gpps; without counters, or through the slot cache, the
+// prefetching 512-thread build stays ahead: config 3 317 vs 301, config 6 with counters 147 vs 142)
+template <int MODE, bool COUNT, bool NODE, int STAGE = 1>
+constexpr bool node_wide() {
+    return NODE && kernel_wpe<MODE, COUNT, NODE, STAGE>() >= 8;
 }
 // STAGE_ + 8 (SINGLE, STAGE 0-2): the table is dst-free (kFlagDstFree: no rule tests dst), so
 // the dst stream is not read
@@ -632,7 +645,7 @@ void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
     constexpr int PF0 = FD ? PG_PREFETCH_FD
                           : (PG_PREFETCH >= 0 ? PG_PREFETCH
                                               : ((MODE == 0 && STAGE != 0 && STAGE != 2 && STAGE != 6) ||
-                                                 (NODE && MODE == 2 && kernel_wpe<MODE, COUNT, NODE>() >= 8)
+                                                 node_wide<MODE, COUNT, NODE, STAGE_>()
                                                      ? 0 : 1));
     constexpr int PF = (!NODE && PF0 == 2) ? 1 : PF0;  // (only node kernels have the gather hook)
     // PD = 2 (PG_PF_DEPTH): the loads run two groups ahead (group q + 2 * stride is
@@ -970,7 +983,7 @@ static void launch_one(const DevTableSet& T, const Tuning& tu, int t, const uint
         // 393.8 -> 471.5 Gpps; config 2's 49 KB blob, three fit: 530 vs 475 at 1024)
         const size_t lds_bytes = hist + (size_t)stage * 4;
         const uint32_t bs = tu.block_stage ? tu.block_stage
-                            : (NODE && MODE == 2 && kernel_wpe<MODE, COUNT, NODE>() >= 8)           ? 1024u
+                            : node_wide<MODE, COUNT, NODE, STAGE>()                                ? 1024u
                             : (MODE == 0 && (STAGE & 7) == 4 && lds_bytes > kLdsPerCU / 3 && PG_FD_BS1024) ? 1024u
                                                                                                      : 512u;
         if (bs == 1024u)
