@@ -644,7 +644,13 @@ void host_q(const DevTableSet& T, bool node, int table_id, const pg_tuple_soa* t
         sp[j] = MODE == 2 ? t->src_port[i + j] : 0u;
     }
     if constexpr (MODE == 0) {
-        classify_q<0, true, Q, PRED>(T, T.blobs, load_tab(T.tabs, table_id), s, d, sp, dp, pr, h, o);
+        const DevTable tab = load_tab(T.tabs, table_id);
+        if ((tab.fsk & kFlagCandI) && (tab.fsk & kFlagDstFree)) {  // the kernels' STAGE 6 walk
+            const DevLoader b{T.blobs + tab.blob_off};
+            classify_candi_q<true, Q>(T, b, b, tab, s, dp, pr, h, o);
+        } else {
+            classify_q<0, true, Q, PRED>(T, T.blobs, tab, s, d, sp, dp, pr, h, o);
+        }
     } else {
         if (node) classify_node_q<MODE, true, Q, PRED, CM>(T, T.node, DevLoader{T.node.img}, s, d, sp, dp, pr, h, o);
         else classify_q<MODE, true, Q, PRED>(T, T.blobs, DevTable{}, s, d, sp, dp, pr, h, o);
