@@ -28,6 +28,11 @@ namespace pg {
 #ifndef PG_AGG_ROUNDS  // wave-aggregation rounds of hit-counter increments (Hist::inc)
 #define PG_AGG_ROUNDS 0
 #endif
+#if defined(PG_PROBE_NOPAIR)  // measurement build only: node evaluations without the PAIR code
+constexpr bool kNodeHasPair = false;
+#else
+constexpr bool kNodeHasPair = true;
+#endif
 #ifndef PG_FD_SKIP  // FD walks over a blob in HBM: no re-read of a finished lane's self word
 #define PG_FD_SKIP 1
 #endif
@@ -629,7 +634,7 @@ struct NodeEval {
             fb[j] = act[j] && !on[j];
             // PAIR table (kNodePairFlag): the pair map entry first, its verdict row after (a
             // uniform test first: node sets without PAIR tables skip this code)
-            pr[j] = N.n_pair && on[j] && (ti.y & kNodePairFlag);
+            pr[j] = kNodeHasPair && N.n_pair && on[j] && (ti.y & kNodePairFlag);
             if (pr[j]) {
                 const uint32_t mo = ti.w & 0xFFFFu;
                 const uint32_t sc = img.u32(mo + ca[j]) & 0xFFFFu, dc = img.u32(mo + cb[j]) >> 16;
@@ -647,7 +652,7 @@ struct NodeEval {
             if (!cm[j]) w[j] = X.u32(pos[j]);
 #endif
         }
-        if (N.n_pair) {
+        if (kNodeHasPair && N.n_pair) {
             PG_UNROLL
             for (int j = 0; j < Q; j++)
                 if (pr[j]) w[j] = X.u32(pv[j] + w[j] * pk[j]);
