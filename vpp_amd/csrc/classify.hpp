@@ -28,11 +28,6 @@ namespace pg {
 #ifndef PG_AGG_ROUNDS  // wave-aggregation rounds of hit-counter increments (Hist::inc)
 #define PG_AGG_ROUNDS 0
 #endif
-#if defined(PG_PROBE_NOPAIR)  // measurement build only: node evaluations without the PAIR code
-constexpr bool kNodeHasPair = false;
-#else
-constexpr bool kNodeHasPair = true;
-#endif
 #ifndef PG_FD_SKIP  // FD walks over a blob in HBM: no re-read of a finished lane's self word
 #define PG_FD_SKIP 1
 #endif
@@ -587,7 +582,8 @@ struct NoHook {
 // (the kernels issue the next quad's stream loads there; see device.hip PG_PREFETCH)
 // CM: the node image's common-row section is in use (device.hpp DevNode): evaluations whose
 // (table, IP class) row is the table's common row read it from the image, not the cross table.
-template <class L, int Q, class H = NoHook, bool CM = false>
+// NP: the node set has no PAIR tables (the launcher's build for it: no PAIR code at all)
+template <class L, int Q, class H = NoHook, bool CM = false, bool NP = false>
 struct NodeEval {
     const DevTableSet& T;
     const DevNode& N;
@@ -634,7 +630,7 @@ struct NodeEval {
             fb[j] = act[j] && !on[j];
             // PAIR table (kNodePairFlag): the pair map entry first, its verdict row after (a
             // uniform test first: node sets without PAIR tables skip this code)
-            pr[j] = kNodeHasPair && N.n_pair && on[j] && (ti.y & kNodePairFlag);
+            pr[j] = !NP && N.n_pair && on[j] && (ti.y & kNodePairFlag);
             if (pr[j]) {
                 const uint32_t mo = ti.w & 0xFFFFu;
                 const uint32_t sc = img.u32(mo + ca[j]) & 0xFFFFu, dc = img.u32(mo + cb[j]) >> 16;
@@ -652,7 +648,7 @@ struct NodeEval {
             if (!cm[j]) w[j] = X.u32(pos[j]);
 #endif
         }
-        if (kNodeHasPair && N.n_pair) {
+        if (!NP && N.n_pair) {
             PG_UNROLL
             for (int j = 0; j < Q; j++)
                 if (pr[j]) w[j] = X.u32(pv[j] + w[j] * pk[j]);
@@ -900,7 +896,8 @@ PG_HD void classify_q(const DevTableSet& T, const uint32_t* blobs, const DevTabl
 
 // Q tuples of one lane, PERPOD / CONN, node path. `img` reads the node image (LDS copy or
 // global memory).
-template <int MODE, bool COUNT, int Q, bool PRED = false, bool CM = false, class L, class HS, class H = NoHook>
+template <int MODE, bool COUNT, int Q, bool PRED = false, bool CM = false, bool NP = false, class L, class HS,
+          class H = NoHook>
 PG_HD void classify_node_q(const DevTableSet& T, const DevNode& N, const L& img, const uint32_t (&s)[Q],
                            const uint32_t (&d)[Q], const uint32_t (&sp)[Q], const uint32_t (&dp)[Q],
                            const uint32_t (&pr)[Q], const HS& h, uint32_t (&out)[Q], const H& hook = H()) {
@@ -971,7 +968,7 @@ PG_HD void classify_node_q(const DevTableSet& T, const DevNode& N, const L& img,
     PG_UNROLL
     for (int j = 0; j < Q; j++) cs[j] = ipc[j], cd[j] = ipc[Q + j];
     bool hooked = false;
-    const NodeEval<L, Q, H, CM> ev{T, N, img, s, d, key, kack, cs, cd, gs, ga, hook, &hooked};
+    const NodeEval<L, Q, H, CM, NP> ev{T, N, img, s, d, key, kack, cs, cd, gs, ga, hook, &hooked};
     if (MODE == 1) {
         int32_t t[Q];
         bool run[Q];

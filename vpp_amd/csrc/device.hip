@@ -440,6 +440,9 @@ constexpr size_t kLdsPerCU = 160u << 10;
 #ifndef PG_CONN_HOT_REGS  // CONN full-histogram build: two hot slots counted in registers
 #define PG_CONN_HOT_REGS 1
 #endif
+#ifndef PG_NODE_NOPAIR  // node sets without PAIR tables: the build without PAIR code (STAGE + 32)
+#define PG_NODE_NOPAIR 1
+#endif
 #ifndef PG_NODE_FULLH  // node kernels whose LDS histogram holds every slot: the specialised build (STAGE + 16)
 #define PG_NODE_FULLH 1
 #endif
@@ -532,6 +535,9 @@ void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
     constexpr bool NODST = MODE == 0 && (STAGE_ & 8);
     // STAGE_ + 16 (node kernels with counters): the LDS histogram holds every slot (launcher)
     constexpr bool FULLH = NODE && COUNT && (STAGE_ & 16);
+    // STAGE_ + 32 (node kernels): the node set has no PAIR tables -- the evaluation carries no
+    // PAIR code (A/B on MI355X: config 5 with counters 118.9 -> 124.7 Gpps, config 3 +1 %)
+    constexpr bool NOPAIR = NODE && (STAGE_ & 32);
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     uint32_t* hist = smem + (STAGE ? stage_words : 0u);
     // node kernels: the LDS histogram, when used, holds every slot (HistT<true>: no window test)
@@ -704,9 +710,9 @@ void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
                 classify_candi_q<COUNT, QC>(T, LdsLoader{}, DevLoader{T.blobs + tab0.blob_off}, tab0, cs, cdp, cpr, h, co);
             } else if constexpr (NODE) {
                 if (c == (PG_HOOK_LAST ? P - QC : 0))
-                    classify_node_q<MODE, COUNT, QC, STAGE && PG_PRED, STAGE == 3>(T, T.node, img, cs, cd, csp, cdp, cpr, h, co, hook);
+                    classify_node_q<MODE, COUNT, QC, STAGE && PG_PRED, STAGE == 3, NOPAIR>(T, T.node, img, cs, cd, csp, cdp, cpr, h, co, hook);
                 else
-                    classify_node_q<MODE, COUNT, QC, STAGE && PG_PRED, STAGE == 3>(T, T.node, img, cs, cd, csp, cdp, cpr, h, co);
+                    classify_node_q<MODE, COUNT, QC, STAGE && PG_PRED, STAGE == 3, NOPAIR>(T, T.node, img, cs, cd, csp, cdp, cpr, h, co);
             } else {
                 classify_q<MODE, COUNT, QC, STAGE == 1 && PG_PRED>(T, blobs, tab0, cs, cd, csp, cdp, cpr, h, co, rootb);
             }
@@ -731,7 +737,7 @@ void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
         else if constexpr (FD) classify_fd_q<COUNT, 1>(T, LdsLoader{}, DevLoader{fd_blob}, tab0, s1, dp1, pr1, h, o);
         else if constexpr (MODE == 0 && STAGE == 6)
             classify_candi_q<COUNT, 1>(T, LdsLoader{}, DevLoader{T.blobs + tab0.blob_off}, tab0, s1, dp1, pr1, h, o);
-        else if constexpr (NODE) classify_node_q<MODE, COUNT, 1, STAGE && PG_PRED, STAGE == 3>(T, T.node, img, s1, d1, sp1, dp1, pr1, h, o);
+        else if constexpr (NODE) classify_node_q<MODE, COUNT, 1, STAGE && PG_PRED, STAGE == 3, NOPAIR>(T, T.node, img, s1, d1, sp1, dp1, pr1, h, o);
         else classify_q<MODE, COUNT, 1, STAGE == 1 && PG_PRED>(T, blobs, tab0, s1, d1, sp1, dp1, pr1, h, o, rootb);
         out[i] = o[0];
     }
@@ -1071,7 +1077,9 @@ static void launch_classify(const DevTableSet& T, const Tuning& tu, int t, const
         };
         // (+ 16: counters in an LDS histogram of every slot, k_classify FULLH)
         const bool full = PG_NODE_FULLH && COUNT && T.n_slots <= kLdsHistMax - 2u;
-        auto go = [&](auto stage, const DevTableSet& Ts, uint32_t words) {
+        // (+ 32: the set has no PAIR tables, k_classify NOPAIR)
+        const bool nopair = T.node.n_pair == 0 && PG_NODE_NOPAIR;
+        auto go1 = [&](auto stage, const DevTableSet& Ts, uint32_t words) {
             constexpr int S = decltype(stage)::value;
             if constexpr (COUNT) {
                 if (full)
@@ -1080,6 +1088,11 @@ static void launch_classify(const DevTableSet& T, const Tuning& tu, int t, const
             }
             launch_one<MODE, COUNT, VEC, S, true>(Ts, tu, t, src, dst, sport, dport, proto, n, out, counters, st, hist,
                                                   cells, words, items);
+        };
+        auto go = [&](auto stage, const DevTableSet& Ts, uint32_t words) {
+            constexpr int S = decltype(stage)::value;
+            if (nopair) return go1(std::integral_constant<int, S + 32>{}, Ts, words);
+            go1(stage, Ts, words);
         };
         if (T.node.cmap && (fits(all) || fits(norec))) {
             const uint32_t w = fits(all) ? all : norec;
