@@ -275,6 +275,18 @@ struct HistT {
     // image: config 6 with counters 99 -> 144 Gpps (A/B on MI355X; 1024 cells 129, 4096 128).
     uint32_t* ckey = nullptr;
     uint32_t cmask = 0, cshift = 32;
+    // one increment of a slot that is never `hot` / `hot2` (the unresolved-interface slot): the
+    // full-histogram builds skip the register tests (their loop-invariant results were hoisted
+    // out of the CONN loop and spilled, each reload a vmcnt(0) wait)
+    PG_HD void inc_cold(uint32_t slot) const {
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(PG_PROBE_NOINC)
+        if constexpr (kFullOnly) {
+            atomicAdd(&lds[slot], 1u);
+            return;
+        }
+#endif
+        inc_t(slot, -1);
+    }
     // one increment of an evaluation of table t (t < 0: no table; its slot is past the rules)
     PG_HD void inc_t(uint32_t slot, int32_t t) const {
 #if defined(__HIP_DEVICE_COMPILE__) && !defined(PG_PROBE_NOINC)
@@ -783,7 +795,7 @@ PG_HD void conn_q(const DevTableSet& T, const EV& ev, const End (&es)[Q], const 
         w[j] = 0;
         if (!live[j]) {
             out[j] = verdict(3u, T.slot_unresolved);
-            if (COUNT) h.inc_t(T.slot_unresolved, -1);
+            if (COUNT) h.inc_cold(T.slot_unresolved);
         }
     }
     // SYN: src interface inbound
@@ -877,7 +889,7 @@ PG_HD void classify_q(const DevTableSet& T, const uint32_t* blobs, const DevTabl
             t[j] = e[j].tout;
             if (!run[j]) {
                 out[j] = verdict(kActFailure, T.slot_unresolved);
-                if (COUNT) h.inc_t(T.slot_unresolved, -1);
+                if (COUNT) h.inc_cold(T.slot_unresolved);
             }
         }
         eval_step<Q, COUNT>(T, ev, t, run, false, h, out);
@@ -979,7 +991,7 @@ PG_HD void classify_node_q(const DevTableSet& T, const DevNode& N, const L& img,
             t[j] = e.tout;
             if (!run[j]) {
                 out[j] = verdict(kActFailure, T.slot_unresolved);
-                if (COUNT) h.inc_t(T.slot_unresolved, -1);
+                if (COUNT) h.inc_cold(T.slot_unresolved);
             }
         }
         eval_step<Q, COUNT>(T, ev, t, run, false, h, out);
