@@ -147,8 +147,9 @@ def test_world_histogram_counts_every_evaluation():
     m = rng.random(len(src)) < 0.6
     src[m] = wd.local_ips[rng.integers(0, len(wd.local_ips), int(m.sum()))]
     conn, slot, hist = wd.conn(src, dst, sport, dport, proto, threads=2, hist=True)
-    _, lt, li, evt, evi = fast.test_connection(wd.acls, wd.if_in, wd.if_out, wd.resolve(src), wd.resolve(dst), src,
-                                               dst, sport, dport, proto, 2, trace=True)
+    sif, dif = wd.conn_ifs(src, dst)
+    _, lt, li, evt, evi = fast.test_connection(wd.acls, wd.if_in, wd.if_out, sif, dif, src, dst, sport, dport, proto,
+                                               2, trace=True)
     made = (evt != -3).sum(axis=1)
     assert made.min() >= 1 and made.max() <= 4 and int(hist.sum()) == int(made.sum())
     direct = np.zeros_like(hist)

@@ -204,7 +204,8 @@ struct End {
 };
 
 // IPv4 -> end point by the iphash (per-table path): a local pod's TAP, else the node-output
-// interface (VXLAN BVI or main; aclengine_mock.go:273-420). One 16-B load per probe step.
+// interface (VXLAN BVI or main; aclengine_mock.go:273-420), marked as a remote pod's or a
+// non-pod address's (device.hpp kEndRemote / kEndInet). One 16-B load per probe step.
 template <int Q>
 PG_HD void probe_q(const DevTableSet& T, const uint32_t (&ip)[Q], End (&e)[Q]) {
     const DevLoader H{T.iphash};
@@ -789,7 +790,13 @@ PG_HD void conn_q(const DevTableSet& T, const EV& ev, const End (&es)[Q], const 
     int32_t t[Q];
     PG_UNROLL
     for (int j = 0; j < Q; j++) {
-        live[j] = es[j].ifc >= 0 && ed[j].ifc >= 0;
+        // both interfaces resolved, and a pair the reference has a Connection* call for: the
+        // end-point kinds (device.hpp kEndRemote / kEndInet) add to less than 3 -- remote pod <->
+        // non-pod and non-pod <-> non-pod fail before any evaluation (aclengine_mock.go:343-347,
+        // 388-392). Interfaces keep their kind bits, so "same interface" (srcIfName == dstIfName)
+        // holds for remote <-> remote, both through the node-output interface.
+        live[j] = es[j].ifc >= 0 && ed[j].ifc >= 0 &&
+                  ((uint32_t)es[j].ifc >> kEndKindShift) + ((uint32_t)ed[j].ifc >> kEndKindShift) < 3u;
         srefl[j] = drefl[j] = false;
         same[j] = es[j].ifc == ed[j].ifc;
         w[j] = 0;

@@ -96,6 +96,17 @@ struct DevNode {
 // slot, 64 KiB with the two extra cells of a SINGLE window)
 constexpr uint32_t kLdsHistCells = 16382;
 
+// End-point kind of an IP-keyed lookup (iphash, node IP classes), in bits 29-28 of a resolved
+// interface index >= 0: a local pod's TAP (0), a pod registered on another node (kEndRemote)
+// or any other address (kEndInet), both of which leave by the node-output interface. The
+// IP-keyed CONN mode picks the reference's Connection* call from the two kinds
+// (aclengine_mock.go:273-420): a remote pod paired with a non-pod address is the "invalid
+// scenario" of ConnectionPodToInternet / ConnectionInternetToPod (:343-347, :388-392) ->
+// FAILURE without an evaluation; non-pod <-> non-pod has no reference call and is FAILURE too
+// (DESIGN.md §1). Kinds add: the pair is valid iff kind(src) + kind(dst) < 3.
+constexpr int32_t kEndRemote = 1 << 28, kEndInet = 2 << 28;
+constexpr uint32_t kEndKindShift = 28;
+
 struct DevTableSet {       // device pointers (valid on the GPU)
     const DevRule* rules;
     const DevTable* tabs;
@@ -103,7 +114,7 @@ struct DevTableSet {       // device pointers (valid on the GPU)
     const int32_t* ifaces; // int2 pairs
     const uint32_t* iphash;// uint4 {ip, iface, in table, out table}
     uint32_t iphash_mask;
-    int32_t node_if;       // interface of non-local IPs, -1 = none (FAILURE)
+    int32_t node_if;       // end point of non-pod IPs: node-output interface | kEndInet, -1 = none (FAILURE)
     int32_t node_in, node_out;  // its ACL tables (-1 = none)
     uint32_t n_rules;      // NR
     uint32_t n_tables;     // T
@@ -193,8 +204,8 @@ void free_analysis(TableAnalysis* an);
 bool build_fd_blob(const TableAnalysis& an, uint32_t dflt, const Tuning& tu, std::vector<uint32_t>& blob,
                    uint32_t max_words, uint32_t lds_words);
 // fastpath.cpp: the node classifier over the tables with an analysis (null = not covered).
-// pods: {IPv4, interface, inbound table, outbound table} of local pods; node_end: the same for
-// every other address. false = over budget (h.node_img left empty).
+// pods: {IPv4, interface (with its kEnd* kind), inbound table, outbound table} of registered
+// pods; node_end: the same for every other address. false = over budget (h.node_img left empty).
 struct NodePod {
     uint32_t ip;
     int32_t ifc, tin, tout;

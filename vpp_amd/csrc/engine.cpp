@@ -356,10 +356,13 @@ void Engine::compile() {
         if (kv.second.second) h.ifaces[2 * i + 1] = table_of_acl[kv.second.second->name];
     }
     std::string nif = node_if_name();
-    h.node_if = nif.empty() ? -1 : iface_index[nif];
-    if (h.node_if >= 0) h.node_in = h.ifaces[2 * h.node_if], h.node_out = h.ifaces[2 * h.node_if + 1];
-    // local pod IP -> {TAP interface, its inbound / outbound tables}; -2 = pod without a
-    // known interface (unresolvable, FAILURE)
+    const int32_t node_ifc = nif.empty() ? -1 : iface_index[nif];
+    if (node_ifc >= 0) h.node_in = h.ifaces[2 * node_ifc], h.node_out = h.ifaces[2 * node_ifc + 1];
+    // end point of every other address: the node-output interface, kind "not a pod"
+    h.node_if = node_ifc >= 0 ? node_ifc | kEndInet : -1;
+    // registered pod IP -> {interface, its inbound / outbound tables}: a local pod's TAP (-2 =
+    // no known interface: unresolvable, FAILURE), a pod on another node the node-output
+    // interface marked kEndRemote (aclengine_mock.go:291-299, 343-347, 388-392)
     struct Ent {
         uint32_t ip;
         int32_t ifc, tin, tout;
@@ -367,7 +370,11 @@ void Engine::compile() {
     std::vector<Ent> ipmap;
     for (auto& kv : pods) {
         Bytes v4;
-        if (kv.second.another_node || !to4(kv.second.ip, &v4)) continue;
+        if (!to4(kv.second.ip, &v4)) continue;
+        if (kv.second.another_node) {  // (no node-output interface: unresolvable like any other address)
+            if (node_ifc >= 0) ipmap.push_back(Ent{ipv4_u32(v4), node_ifc | kEndRemote, h.node_in, h.node_out});
+            continue;
+        }
         std::string ifn;
         Ent e{ipv4_u32(v4), -2, -1, -1};
         if (ifaces.if_name(kv.first, &ifn)) {

@@ -123,6 +123,7 @@ class Engine:
         if not self.h:
             raise PolicyError(_capi.PG_ENOMEM, "pg_create failed")
         self._keep = []
+        self.registered_pods = {}  # "ns/name" -> (IP, anotherNode) as given to RegisterPod
 
     def close(self):
         if self.h:
@@ -190,6 +191,7 @@ class Engine:
     def RegisterPod(self, pod, ip, another_node):
         ns, name = _pod(pod)
         self._ck(lib.pg_register_pod(self.h, _b(ns), _b(name), _b(ip), int(another_node)))
+        self.registered_pods["%s/%s" % (ns, name)] = (ip, bool(another_node))
 
     # ACL install / introspection
     def ApplyTxn(self, resync, ops):
