@@ -246,6 +246,10 @@ int pg_debug_walk_blob(pg_ctx* ctx, const char* acl_name, const uint32_t* src, c
  * Does not touch the device. */
 int pg_debug_classify_host(pg_ctx* ctx, int mode, int table_id, const pg_tuple_soa* tuples, uint64_t n,
                            uint32_t* out, uint64_t* counters, int flags);
+/* TESTS ONLY -- never on the classify path: install n host counters (e.g. from
+ * pg_debug_classify_host) as the LOCAL or CLUSTER snapshot in the currently compiled slot layout,
+ * so the snapshot readers below can be tested without a GPU. n must equal the slot count. */
+int pg_debug_set_snapshot(pg_ctx* ctx, int which, const uint64_t* counters, size_t n);
 /* TESTS / MEASUREMENT ONLY -- never on the classify path: per tuple, the loads a SINGLE-mode
  * launch on table_id makes of the table's classification structure, split by where the launch
  * finds the word: lds_reads (the LDS-staged part) and mem_reads (HBM / L2 gathers; rule reads of
@@ -281,13 +285,36 @@ int pg_stream_probe(pg_ctx* ctx, int fields, const pg_tuple_soa* tuples, uint64_
 uint64_t* pg_counters_device(pg_ctx* ctx);
 int pg_reset_counters(pg_ctx* ctx, void* hip_stream);
 /* waits for this context's classify launches, copies min(n, slots) counters -> slots copied
- * (also refreshes the host snapshot) */
+ * (also refreshes the LOCAL host snapshot) */
 int pg_read_counters(pg_ctx* ctx, uint64_t* host_out, size_t n);
-/* the host snapshot of the counters taken by the last pg_read_counters / pg_allreduce_counters*
- * (cluster-wide after an all-reduce); never touches the GPU, so a pull-style statscollector
- * gauge (RegisterGaugeFunc, plugin_impl_statscollector.go:248-261) can read it at scrape time.
- * Copies min(n, slots) -> number of slots in the snapshot (0 before the first read). */
+/* ---- host snapshots: the statscollector value source -----------------------------------
+ * (RegisterGaugeFunc, plugin_impl_statscollector.go:248-261: a pull-style gauge whose value
+ * function runs at scrape time, on its own goroutine.) The library keeps two host copies of the
+ * counters, each with the slot layout it was counted in; reading them never touches the GPU and
+ * is safe from any thread while the context classifies:
+ *   PG_SNAP_LOCAL    this GPU's counts, as of the last pg_read_counters
+ *   PG_SNAP_CLUSTER  the sum over the communicator, as of the last pg_allreduce_counters*
+ *   PG_SNAP_GAUGE    CLUSTER once the context has a communicator, else LOCAL: a monotonic
+ *                    source either way (neither call writes the other's copy)
+ * Slots are renumbered whenever the tables are recompiled (and the counters restart from
+ * zero), so a gauge should be keyed by a stable rule identity -- (ACL name, rule index) -- and
+ * read with pg_counter_of_rule, which resolves it in the snapshot's own layout. */
+enum { PG_SNAP_GAUGE = 0, PG_SNAP_LOCAL = 1, PG_SNAP_CLUSTER = 2 };
+/* PG_SNAP_GAUGE snapshot: copies min(n, slots) -> number of slots in it (0 before the first read) */
 int pg_counters_snapshot(const pg_ctx* ctx, uint64_t* host_out, size_t n);
+/* slots [first, first + n) of a snapshot (clipped to its size) -> number copied; *layout_gen
+ * (optional) = the layout generation of that snapshot (0: none taken yet) */
+int pg_counters_snapshot_range(const pg_ctx* ctx, int which, uint32_t first, uint32_t n, uint64_t* host_out,
+                               uint64_t* layout_gen);
+/* one rule's count in a snapshot by its stable identity: ACL name and rule index (-1: the ACL's
+ * default deny); acl_name NULL with rule_index -1 = the "no ACL" slot, -2 = the unresolved-
+ * interface slot. O(log ACLs), no allocation. PG_ENOENT: no snapshot yet, or the ACL / index
+ * does not exist in the snapshot's layout. *layout_gen (optional) as above. */
+int pg_counter_of_rule(const pg_ctx* ctx, int which, const char* acl_name, int rule_index, uint64_t* value,
+                       uint64_t* layout_gen);
+/* generation of the compiled slot layout (increments on every recompile; 0 = never compiled):
+ * an agent re-registers gauges for new (ACL, rule) identities when it changes */
+uint64_t pg_counter_layout_gen(const pg_ctx* ctx);
 
 /* ---- RCCL over xGMI: per-rule hit counters summed over the GPUs of a node -------------
  * (the statscollector path). The classify path itself has no exchange.

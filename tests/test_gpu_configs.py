@@ -18,6 +18,7 @@ from oracle import fast, gen
 
 pytestmark = pytest.mark.gpu
 
+from vpp_amd import _capi  # noqa: E402
 from vpp_amd import device as D  # noqa: E402
 from vpp_amd import renderer as R  # noqa: E402
 from vpp_amd import workloads as W  # noqa: E402
@@ -280,6 +281,19 @@ def test_rccl_counter_allreduce_single_rank():
     # a second reduction (a periodic gauge) sums the same local counts again: no compounding,
     # and the local counters are still this rank's own
     assert np.array_equal(D.allreduce_counters(e), hist) and np.array_equal(D.read_counters(e), hist)
+    # with a communicator the gauge snapshot is the cluster sum: a later pg_read_counters (this
+    # rank's own, now ahead of the last reduction) refreshes only the LOCAL snapshot, so the
+    # gauge never jumps between local and summed counts (a monotonic source)
+    D.classify(e, MODE_SINGLE, tid, b, out, counters=D.counters_device_ptr(e))
+    assert np.array_equal(D.read_counters(e), 2 * hist)
+    assert np.array_equal(D.counters_snapshot(e), hist)
+    assert np.array_equal(D.counters_snapshot_range(e, _capi.SNAP_LOCAL, 0, len(hist))[0], 2 * hist)
+    assert np.array_equal(D.counters_snapshot_range(e, _capi.SNAP_CLUSTER, 0, len(hist))[0], hist)
+    base, nr, dflt = e.table_info(tid)
+    for i in range(nr):
+        assert D.counter_of_rule(e, _capi.SNAP_GAUGE, "x", i)[0] == hist[base + i]
+    assert D.counter_of_rule(e, _capi.SNAP_GAUGE, "x", -1)[0] == hist[dflt]
+    assert np.array_equal(D.allreduce_counters(e), 2 * hist) and np.array_equal(D.counters_snapshot(e), 2 * hist)
     assert torch.cuda.current_device() == 0
     e2, _ = _small_engine(10)
     D.comm_init_all([e2])

@@ -1,5 +1,6 @@
 #!/bin/bash
 # The host-threading tests (tests/test_threads_host.py: contexts driven from several OS threads at
+# once, and the counter snapshots read by gauge threads while replaced, test_stats_host.py)
 # once, the way cgo callers may) against the TSan build of the host C++ layer
 # (make -C vpp_amd/csrc tsan). Any data-race report fails the run (halt_on_error).
 #   bash tools/tsan_tests.sh [pytest args]
@@ -9,4 +10,4 @@ make -s -j8 -C "$R/vpp_amd/csrc" tsan || exit 1
 export VPP_AMD_LIB=$R/vpp_amd/libpolicygpu_tsan.so
 export LD_PRELOAD=$(gcc -print-file-name=libtsan.so)
 export TSAN_OPTIONS="halt_on_error=1 exitcode=66 report_signal_unsafe=0 ignore_noninstrumented_modules=1 ${TSAN_LOG:+log_path=$TSAN_LOG}"
-cd "$R" && python -m pytest tests/test_threads_host.py -x -q -s -p no:cacheprovider ${*}
+cd "$R" && python -m pytest tests/test_threads_host.py tests/test_stats_host.py::test_snapshot_readers_race_a_writer -x -q -s -p no:cacheprovider ${*}

@@ -106,6 +106,8 @@ class pg_session_rule(C.Structure):
                 ("appns_index", C.c_uint32), ("scope", C.c_uint8), ("tag", C.c_char * 64)]
 
 
+SNAP_GAUGE, SNAP_LOCAL, SNAP_CLUSTER = 0, 1, 2  # pg_counters_snapshot_range / pg_counter_of_rule
+
 _P = C.c_void_p
 _SIGS = {
     "pg_version": (C.c_char_p, []),
@@ -116,6 +118,11 @@ _SIGS = {
     "pg_ctx_get_tuning": (C.c_int, [_P, C.c_char_p, C.POINTER(C.c_int)]),
     "pg_ctx_device": (C.c_int, [_P]),
     "pg_counters_snapshot": (C.c_int, [_P, C.POINTER(C.c_uint64), C.c_size_t]),
+    "pg_counters_snapshot_range": (C.c_int, [_P, C.c_int, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint64),
+                                             C.POINTER(C.c_uint64)]),
+    "pg_counter_of_rule": (C.c_int, [_P, C.c_int, C.c_char_p, C.c_int, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
+    "pg_counter_layout_gen": (C.c_uint64, [_P]),
+    "pg_debug_set_snapshot": (C.c_int, [_P, C.c_int, C.POINTER(C.c_uint64), C.c_size_t]),
     "pg_comm_unique_id": (C.c_int, [C.c_char_p]),
     "pg_comm_init_rank": (C.c_int, [_P, C.c_int, C.c_char_p, C.c_int]),
     "pg_comm_init_all": (C.c_int, [C.POINTER(_P), C.c_int]),

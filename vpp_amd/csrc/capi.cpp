@@ -626,6 +626,7 @@ DevTableSet host_view(const HostTableSet& h) {
     v.slot_noacl = v.n_rules + v.n_tables;
     v.slot_unresolved = v.slot_noacl + 1;
     v.n_slots = v.slot_unresolved + 1;
+    v.slot_hot_in = h.slot_hot_in;
     v.node = h.node;
     v.node.img = h.node_img.empty() ? nullptr : h.node_img.data();
     v.node.cross = h.node_img.empty() ? nullptr : h.node_cross.data();
@@ -699,6 +700,20 @@ int pg_debug_classify_host(pg_ctx* ctx, int mode, int table_id, const pg_tuple_s
     GUARD_END(ctx)
 }
 
+int pg_debug_set_snapshot(pg_ctx* ctx, int which, const uint64_t* counters, size_t n) {
+    if (!ctx || (!counters && n) || (which != PG_SNAP_LOCAL && which != PG_SNAP_CLUSTER)) return PG_EINVAL;
+    GUARD_BEGIN
+    Engine& E = ctx->eng;
+    if (!E.compiled) E.compile();
+    if (n != E.layout->slots) return fail(ctx, PG_EINVAL, "counter count differs from the compiled slots");
+    std::lock_guard<std::mutex> lk(E.snap_mu);
+    CounterSnapshot& s = which == PG_SNAP_LOCAL ? E.snap_local : E.snap_cluster;
+    s.v.assign(counters, counters + n);
+    s.layout = E.layout;
+    return PG_OK;
+    GUARD_END(ctx)
+}
+
 int pg_node_stats(pg_ctx* ctx, uint32_t* ip_classes, uint32_t* key_classes, uint64_t* image_bytes,
                   uint64_t* cross_bytes) {
     if (!ctx) return PG_EINVAL;
@@ -741,7 +756,7 @@ int pg_node_list_stats(pg_ctx* ctx, uint64_t* record_bytes, int* in_image) {
     if (!E.compiled) E.compile();
     const HostTableSet& h = E.host;
     if (h.node_img.empty()) return fail(ctx, PG_ENOENT, "no node classifier (disabled or over budget)");
-    if (record_bytes) *record_bytes = ((uint64_t)h.node_cross.size() - h.node.rec0) * 4;
+    if (record_bytes) *record_bytes = (uint64_t)h.node_rec_words * 4;
     if (in_image) *in_image = h.node.lrec != 0;
     return PG_OK;
     GUARD_END(ctx)
@@ -829,20 +844,79 @@ int pg_read_counters(pg_ctx* ctx, uint64_t* host_out, size_t n) {
     int rc = E.sync();
     if (rc) return rc;
     std::string err;
-    E.snapshot.resize(E.counter_slots);
+    std::vector<uint64_t> v(E.counter_slots);
     // the launches of this context that count have completed (their streams' events), then copy
-    if (dev_wait_uses(E.cur, &err) != 0 || dev_copy_d2h(E.snapshot.data(), E.counters, E.counter_slots * 8, &err) != 0)
+    if (dev_wait_uses(E.cur, &err) != 0 || dev_copy_d2h(v.data(), E.counters, E.counter_slots * 8, &err) != 0)
         return fail(ctx, PG_EIO, err);
     size_t k = std::min(n, E.counter_slots);
-    std::memcpy(host_out, E.snapshot.data(), k * 8);
+    std::memcpy(host_out, v.data(), k * 8);
+    std::lock_guard<std::mutex> lk(E.snap_mu);
+    E.snap_local.v.swap(v);
+    E.snap_local.layout = E.layout;
     return (int)k;
+}
+
+// the snapshot a `which` names (PG_SNAP_*); the gauge's: the cluster sum once a communicator exists
+static const CounterSnapshot* pick_snapshot(const Engine& E, int which) {
+    if (which == PG_SNAP_GAUGE) which = E.comm ? PG_SNAP_CLUSTER : PG_SNAP_LOCAL;
+    if (which == PG_SNAP_LOCAL) return &E.snap_local;
+    if (which == PG_SNAP_CLUSTER) return &E.snap_cluster;
+    return nullptr;
 }
 
 int pg_counters_snapshot(const pg_ctx* ctx, uint64_t* host_out, size_t n) {
     if (!ctx || (!host_out && n)) return PG_EINVAL;
-    const size_t k = std::min(n, ctx->eng.snapshot.size());
-    if (k) std::memcpy(host_out, ctx->eng.snapshot.data(), k * 8);
-    return (int)ctx->eng.snapshot.size();
+    const Engine& E = ctx->eng;
+    std::lock_guard<std::mutex> lk(E.snap_mu);
+    const CounterSnapshot* s = pick_snapshot(E, PG_SNAP_GAUGE);
+    const size_t k = std::min(n, s->v.size());
+    if (k) std::memcpy(host_out, s->v.data(), k * 8);
+    return (int)s->v.size();
+}
+
+int pg_counters_snapshot_range(const pg_ctx* ctx, int which, uint32_t first, uint32_t n, uint64_t* host_out,
+                               uint64_t* layout_gen) {
+    if (!ctx || (!host_out && n)) return PG_EINVAL;
+    const Engine& E = ctx->eng;
+    std::lock_guard<std::mutex> lk(E.snap_mu);
+    const CounterSnapshot* s = pick_snapshot(E, which);
+    if (!s) return PG_EINVAL;
+    if (layout_gen) *layout_gen = s->layout ? s->layout->gen : 0;
+    const size_t sz = s->v.size();
+    const size_t k = first >= sz ? 0 : std::min<size_t>(n, sz - first);
+    if (k) std::memcpy(host_out, s->v.data() + first, k * 8);
+    return (int)k;
+}
+
+int pg_counter_of_rule(const pg_ctx* ctx, int which, const char* acl_name, int rule_index, uint64_t* value,
+                       uint64_t* layout_gen) {
+    if (!ctx || !value || rule_index < -2) return PG_EINVAL;
+    const Engine& E = ctx->eng;
+    std::lock_guard<std::mutex> lk(E.snap_mu);
+    const CounterSnapshot* s = pick_snapshot(E, which);
+    if (!s) return PG_EINVAL;
+    if (!s->layout) return PG_ENOENT;  // no snapshot taken yet
+    const SlotLayout& L = *s->layout;
+    if (layout_gen) *layout_gen = L.gen;
+    uint32_t slot;
+    if (!acl_name) {
+        if (rule_index == -1) slot = L.noacl;
+        else if (rule_index == -2) slot = L.unresolved;
+        else return PG_EINVAL;
+    } else {
+        auto it = L.tabs.find(acl_name);
+        if (it == L.tabs.end() || rule_index < -1 || (rule_index >= 0 && (uint32_t)rule_index >= it->second.n))
+            return PG_ENOENT;
+        slot = rule_index < 0 ? it->second.dflt : it->second.base + (uint32_t)rule_index;
+    }
+    if (slot >= s->v.size()) return PG_ENOENT;
+    *value = s->v[slot];
+    return PG_OK;
+}
+
+uint64_t pg_counter_layout_gen(const pg_ctx* ctx) {
+    if (!ctx) return 0;
+    return ctx->eng.layout ? ctx->eng.layout->gen : 0;
 }
 
 // ---- RCCL: per-rule hit counters summed over GPUs --------------------------
@@ -980,10 +1054,13 @@ static int allreduce_counters(pg_ctx* const* ctxs, int k, void* const* streams) 
         return fail(ctxs[0], PG_EIO, err);
     for (int i = 0; i < k; i++) {
         Engine& E = ctxs[i]->eng;
-        E.snapshot.resize(E.counter_slots);
+        std::vector<uint64_t> v(E.counter_slots);
         if (dev_set_device(E.device, &err) != 0 || dev_stream_sync(sts[i], &err) != 0 ||
-            dev_copy_d2h(E.snapshot.data(), E.reduced, E.counter_slots * 8, &err) != 0)
+            dev_copy_d2h(v.data(), E.reduced, E.counter_slots * 8, &err) != 0)
             return fail(ctxs[i], PG_EIO, err);
+        std::lock_guard<std::mutex> lk(E.snap_mu);
+        E.snap_cluster.v.swap(v);
+        E.snap_cluster.layout = E.layout;
     }
     return PG_OK;
 }

@@ -118,13 +118,23 @@ int dev_mark_use(DeviceBuffers* b, void* stream, bool fenced, std::string* err) 
     // bounded list: past kMaxUses streams, wait for the recorded launches and start over
     constexpr size_t kMaxUses = 32;
     if (b->uses.size() >= kMaxUses) {
+        // wait for every recorded launch (keeping the first error), then destroy every event and
+        // clear the list on both paths, so no destroyed event stays listed
+        hipError_t first = hipSuccess;
         for (auto& u : b->uses) {
-            if (u.plain_rec) HIPCHK(hipEventSynchronize(u.plain));
-            if (u.fenced_rec) HIPCHK(hipEventSynchronize(u.fenced));
+            hipError_t e1 = u.plain_rec ? hipEventSynchronize(u.plain) : hipSuccess;
+            hipError_t e2 = u.fenced_rec ? hipEventSynchronize(u.fenced) : hipSuccess;
+            if (first == hipSuccess) first = e1 != hipSuccess ? e1 : e2;
+        }
+        for (auto& u : b->uses) {
             (void)hipEventDestroy(u.plain);
             (void)hipEventDestroy(u.fenced);
         }
         b->uses.clear();
+        if (first != hipSuccess) {
+            if (err) *err = std::string("hipEventSynchronize: ") + hipGetErrorString(first);
+            return -1;
+        }
     }
     DeviceBuffers::Use u{s, nullptr, nullptr, false, false};
     HIPCHK(hipEventCreateWithFlags(&u.plain, hipEventDisableTiming | hipEventDisableSystemFence));
@@ -198,15 +208,7 @@ DeviceBuffers* dev_upload(const HostTableSet& h, std::string* err) {
     v.slot_noacl = v.n_rules + v.n_tables;
     v.slot_unresolved = v.slot_noacl + 1;
     v.n_slots = v.slot_unresolved + 1;
-    {
-        std::vector<uint32_t> uses(h.tabs.size(), 0);
-        for (size_t i = 0; i + 1 < h.ifaces.size(); i += 2)
-            if (h.ifaces[i] >= 0 && (size_t)h.ifaces[i] < uses.size()) uses[h.ifaces[i]]++;
-        v.slot_hot_in = 0xFFFFFFFFu;
-        uint32_t best = 1;  // shared by two interfaces at least
-        for (size_t t = 0; t < uses.size(); t++)
-            if (uses[t] > best && h.tabs[t].n_rules) best = uses[t], v.slot_hot_in = h.tabs[t].rule_base + h.tabs[t].n_rules - 1u;
-    }
+    v.slot_hot_in = h.slot_hot_in;
     v.node = h.node;
     v.node.img = h.node_img.empty() ? nullptr : (const uint32_t*)(base + o_nimg);
     v.node.cross = h.node_img.empty() ? nullptr : (const uint32_t*)(base + o_nx);

@@ -143,8 +143,10 @@ struct HostTableSet {
     std::vector<uint32_t> iphash;
     uint32_t iphash_mask = 0;
     int32_t node_if = -1, node_in = -1, node_out = -1;
+    uint32_t slot_hot_in = 0xFFFFFFFFu;          // DevTableSet.slot_hot_in (engine.cpp compile)
     std::vector<uint32_t> node_img, node_cross;  // empty img: no node classifier
     DevNode node{};                              // header fields (pointers unset)
+    uint32_t node_rec_words = 0;                 // words of the node's dst records (build_node)
 };
 
 // table blobs up to this many words are staged in LDS by default (64 KiB); larger ones are

@@ -340,6 +340,16 @@ void Engine::compile() {
         fnv(table_names[t].data(), table_names[t].size() + 1);
         fnv(&h.tabs[t].n_rules, 4);
     }
+    {
+        auto L = std::make_shared<SlotLayout>();
+        L->gen = ++layout_gen;
+        for (uint32_t t = 0; t < T; t++)
+            L->tabs[table_names[t]] = SlotLayout::Tab{h.tabs[t].rule_base, h.tabs[t].n_rules, NR + t};
+        L->noacl = NR + T;
+        L->unresolved = NR + T + 1;
+        L->slots = NR + T + 2;
+        layout = std::move(L);
+    }
 
     // interfaces
     iface_index.clear();
@@ -360,6 +370,18 @@ void Engine::compile() {
     if (node_ifc >= 0) h.node_in = h.ifaces[2 * node_ifc], h.node_out = h.ifaces[2 * node_ifc + 1];
     // end point of every other address: the node-output interface, kind "not a pod"
     h.node_if = node_ifc >= 0 ? node_ifc | kEndInet : -1;
+    // the last rule of the inbound ACL the most interfaces share (at least two; the renderer's
+    // reflective ACL): CONN kernels count it in a register (device.hpp slot_hot_in)
+    {
+        std::vector<uint32_t> uses(h.tabs.size(), 0);
+        for (size_t i = 0; i + 1 < h.ifaces.size(); i += 2)
+            if (h.ifaces[i] >= 0 && (size_t)h.ifaces[i] < uses.size()) uses[h.ifaces[i]]++;
+        h.slot_hot_in = 0xFFFFFFFFu;
+        uint32_t best = 1;
+        for (size_t t = 0; t < uses.size(); t++)
+            if (uses[t] > best && h.tabs[t].n_rules)
+                best = uses[t], h.slot_hot_in = h.tabs[t].rule_base + h.tabs[t].n_rules - 1u;
+    }
     // registered pod IP -> {interface, its inbound / outbound tables}: a local pod's TAP (-2 =
     // no known interface: unresolvable, FAILURE), a pod on another node the node-output
     // interface marked kEndRemote (aclengine_mock.go:291-299, 343-347, 388-392)

@@ -4,6 +4,8 @@
 // evalACL/testConnection on the GPU.
 #pragma once
 #include <map>
+#include <memory>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -15,6 +17,25 @@ namespace pg {
 struct PodReg {
     Bytes ip;
     bool another_node = false;
+};
+
+// The counter-slot layout of one compiled table set, kept with every host snapshot of the
+// counters, so a statscollector gauge keyed by a stable rule identity (ACL name, rule index)
+// reads the slot that identity had in the snapshot it reads (slots are renumbered on every
+// recompile).
+struct SlotLayout {
+    uint64_t gen = 0;  // Engine::layout_gen when compiled
+    struct Tab {
+        uint32_t base, n, dflt;
+    };
+    std::map<std::string, Tab> tabs;  // ACL name -> its slots
+    uint32_t noacl = 0, unresolved = 0, slots = 0;
+};
+
+// A host copy of the counters and the layout they were counted in.
+struct CounterSnapshot {
+    std::vector<uint64_t> v;
+    std::shared_ptr<const SlotLayout> layout;  // null: never taken
 };
 
 // Compiled form of one vpp_acl rule (evalACL semantics, aclengine_mock.go:510-649).
@@ -56,9 +77,15 @@ struct Engine {
     // local counts stay this rank's and repeated reductions do not compound
     unsigned long long* reduced = nullptr;
     size_t reduced_slots = 0;
-    // host copy of the counters as last all-reduced / read (pg_counters_snapshot: the
-    // statscollector gauge reads it without touching the GPU)
-    std::vector<uint64_t> snapshot;
+    // slot layout of the compiled set; layout_gen counts the recompiles that renumbered slots
+    std::shared_ptr<const SlotLayout> layout;
+    uint64_t layout_gen = 0;
+    // host copies of the counters, read by the statscollector gauges without touching the GPU
+    // (pg_counters_snapshot*): this rank's own as of the last pg_read_counters, and the sum over
+    // the communicator as of the last pg_allreduce_counters*. Gauges run on their own threads
+    // (scrape time), so the snapshots sit behind snap_mu.
+    mutable std::mutex snap_mu;
+    CounterSnapshot snap_local, snap_cluster;
 
     ~Engine();
     std::string apply_txn(bool resync, const AclOps& ops);

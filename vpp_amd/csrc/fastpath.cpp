@@ -895,6 +895,7 @@ bool build_node(HostTableSet& h, const std::vector<TableAnalysis*>& an, const st
     h.node_img.clear();
     h.node_cross.clear();
     h.node = DevNode{};
+    h.node_rec_words = 0;
     const uint32_t T = (uint32_t)h.tabs.size();
     if (!tu.node_build || T == 0 || T >= 0xFFFFu) return false;
     std::vector<uint32_t> cov;
@@ -1112,6 +1113,7 @@ bool build_node(HostTableSet& h, const std::vector<TableAnalysis*>& an, const st
     // +17 % with the lists not walked at all, measured); launches that do not stage them read
     // the cross-array copy (device.hip)
     N.rec0 = (uint32_t)rec0;
+    h.node_rec_words = (uint32_t)recs.size();
     N.lrec = 0;
     if (!recs.empty() && recs.size() <= tu.node_list_words) {
         while (img.size() % 4) img.push_back(0);

@@ -123,11 +123,38 @@ def reset_counters(engine, stream=None):
 
 
 def counters_snapshot(engine):
-    """host snapshot of the last read / all-reduce (pg_counters_snapshot: no GPU access)"""
+    """the gauge snapshot (pg_counters_snapshot: the cluster sum once a communicator exists,
+    else this GPU's counts as of the last read; no GPU access)"""
     n = engine._ck(lib.pg_counters_snapshot(engine.h, None, 0))
     buf = (C.c_uint64 * max(1, n))()
     engine._ck(lib.pg_counters_snapshot(engine.h, buf, n))
     return np.frombuffer(buf, dtype=np.uint64)[:n].copy()
+
+
+def counters_snapshot_range(engine, which, first, n):
+    """slots [first, first + n) of a host snapshot (SNAP_LOCAL / SNAP_CLUSTER / SNAP_GAUGE)
+    -> (u64 array, its layout generation); no GPU access"""
+    buf = (C.c_uint64 * max(1, n))()
+    gen = C.c_uint64()
+    k = engine._ck(lib.pg_counters_snapshot_range(engine.h, which, first, n, buf, C.byref(gen)))
+    return np.frombuffer(buf, dtype=np.uint64)[:k].copy(), gen.value
+
+
+def counter_of_rule(engine, which, acl_name, rule_index):
+    """one rule's count in a host snapshot by (ACL name, rule index; -1 = default deny; name
+    None: -1 "no ACL", -2 unresolved) resolved in that snapshot's layout -> (value, layout
+    generation), or None when the snapshot has no such rule; no GPU access"""
+    v, gen = C.c_uint64(), C.c_uint64()
+    rc = lib.pg_counter_of_rule(engine.h, which, acl_name.encode() if acl_name is not None else None, rule_index,
+                                C.byref(v), C.byref(gen))
+    if rc == _capi.PG_ENOENT:
+        return None
+    engine._ck(rc)
+    return v.value, gen.value
+
+
+def counter_layout_gen(engine):
+    return lib.pg_counter_layout_gen(engine.h)
 
 
 # ---- RCCL counter all-reduce through the C ABI (include/policygpu.h pg_comm_*) -------------
