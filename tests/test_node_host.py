@@ -83,6 +83,11 @@ def check(e, local, tup, expect_node=True):
     # fit their LDS budget): same verdicts and counters
     p0, c0 = e.debug_classify_host(MODE_PERPOD, -1, *tup, counters=True, node=True, common=False)
     assert np.array_equal(p0, pn) and np.array_equal(c0, cpn)
+    # PERPOD with dst's end point from the end-point window (nodes without PAIR tables; the
+    # flag is ignored otherwise): same verdicts and counters, with and without common rows
+    for cm in (True, False):
+        pe, ce = e.debug_classify_host(MODE_PERPOD, -1, *tup, counters=True, node=True, common=cm, epwin=True)
+        assert np.array_equal(pe, pn) and np.array_equal(ce, cpn)
     q0, d0 = e.debug_classify_host(MODE_CONN, -1, *tup, counters=True, node=True, common=False)
     q1, d1 = e.debug_classify_host(MODE_CONN, -1, *tup, counters=True, node=True)
     assert np.array_equal(q0, q1) and np.array_equal(d0, d1)
@@ -179,6 +184,11 @@ def test_config3_cluster_node_path():
     assert np.array_equal(got >> 30, conn.astype(np.uint32)) and np.array_equal(got & 0x3FFFFFFF, cslot)
     got0 = e.debug_classify_host(MODE_CONN, -1, src, dst, sport, dport, proto, node=True, common=False)
     assert np.array_equal(got0, got)
+    # the PERPOD end-point window: every local pod between 10.1.0.1 and 10.1.9.90, u8 codes
+    assert ns["ep_window_addresses"] == (9 << 8) + 90 and not ns["ep_window_wide"], ns
+    assert ns["ep_window_base"] == W.ip_u32("10.1.0.1"), ns
+    got = e.debug_classify_host(MODE_PERPOD, -1, src, dst, sport, dport, proto, node=True, epwin=True)
+    assert np.array_equal(got >> 30, act.astype(np.uint32)) and np.array_equal(got & 0x3FFFFFFF, slot)
     # the global table's dst-specific rules: dst records, a copy at the end of the image
     assert ns["list_record_bytes"] > 0 and ns["list_records_in_image"], ns
 
@@ -219,7 +229,8 @@ def test_common_rows_disabled():
         e2, local2, pod_ips2 = topology(random.Random(77))
         ns2 = e2.node_stats()
         recs = ns2["list_record_bytes"] if ns2["list_records_in_image"] else 0
-        assert ns2["common_row_pairs"] == 0 and ns2["image_bytes"] == ns2["base_image_bytes"] + recs
+        win = (ns2["ep_window_addresses"] * (2 if ns2["ep_window_wide"] else 1) + 15) // 16 * 16
+        assert ns2["common_row_pairs"] == 0 and ns2["image_bytes"] == ns2["base_image_bytes"] + recs + win
         assert np.array_equal(e2.debug_classify_host(MODE_CONN, -1, *tup, node=True), on)
     finally:
         assert _capi.lib.pg_set_tuning(b"node_common", 1) == 0

@@ -445,6 +445,9 @@ constexpr size_t kLdsPerCU = 160u << 10;
 #ifndef PG_NODE_NOPAIR  // node sets without PAIR tables: the build without PAIR code (STAGE + 32)
 #define PG_NODE_NOPAIR 1
 #endif
+#ifndef PG_NODE_EPWIN  // PERPOD over such sets: dst's end point from the end-point window (STAGE + 64)
+#define PG_NODE_EPWIN 1
+#endif
 #ifndef PG_NODE_FULLH  // node kernels whose LDS histogram holds every slot: the specialised build (STAGE + 16)
 #define PG_NODE_FULLH 1
 #endif
@@ -540,6 +543,9 @@ void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
     // STAGE_ + 32 (node kernels): the node set has no PAIR tables -- the evaluation carries no
     // PAIR code (A/B on MI355X: config 5 with counters 118.9 -> 124.7 Gpps, config 3 +1 %)
     constexpr bool NOPAIR = NODE && (STAGE_ & 32);
+    // STAGE_ + 64 (PERPOD, no PAIR tables, the image staged with its end-point window): dst's
+    // end point from the window instead of its trie walk (DevNode ep_*)
+    constexpr bool EPWIN = NODE && MODE == 1 && NOPAIR && (STAGE_ & 64);
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     uint32_t* hist = smem + (STAGE ? stage_words : 0u);
     // node kernels: the LDS histogram, when used, holds every slot (HistT<true>: no window test)
@@ -712,9 +718,9 @@ void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
                 classify_candi_q<COUNT, QC>(T, LdsLoader{}, DevLoader{T.blobs + tab0.blob_off}, tab0, cs, cdp, cpr, h, co);
             } else if constexpr (NODE) {
                 if (c == (PG_HOOK_LAST ? P - QC : 0))
-                    classify_node_q<MODE, COUNT, QC, STAGE && PG_PRED, STAGE == 3, NOPAIR>(T, T.node, img, cs, cd, csp, cdp, cpr, h, co, hook);
+                    classify_node_q<MODE, COUNT, QC, STAGE && PG_PRED, STAGE == 3, NOPAIR, EPWIN>(T, T.node, img, cs, cd, csp, cdp, cpr, h, co, hook);
                 else
-                    classify_node_q<MODE, COUNT, QC, STAGE && PG_PRED, STAGE == 3, NOPAIR>(T, T.node, img, cs, cd, csp, cdp, cpr, h, co);
+                    classify_node_q<MODE, COUNT, QC, STAGE && PG_PRED, STAGE == 3, NOPAIR, EPWIN>(T, T.node, img, cs, cd, csp, cdp, cpr, h, co);
             } else {
                 classify_q<MODE, COUNT, QC, STAGE == 1 && PG_PRED>(T, blobs, tab0, cs, cd, csp, cdp, cpr, h, co, rootb);
             }
@@ -739,7 +745,7 @@ void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
         else if constexpr (FD) classify_fd_q<COUNT, 1>(T, LdsLoader{}, DevLoader{fd_blob}, tab0, s1, dp1, pr1, h, o);
         else if constexpr (MODE == 0 && STAGE == 6)
             classify_candi_q<COUNT, 1>(T, LdsLoader{}, DevLoader{T.blobs + tab0.blob_off}, tab0, s1, dp1, pr1, h, o);
-        else if constexpr (NODE) classify_node_q<MODE, COUNT, 1, STAGE && PG_PRED, STAGE == 3, NOPAIR>(T, T.node, img, s1, d1, sp1, dp1, pr1, h, o);
+        else if constexpr (NODE) classify_node_q<MODE, COUNT, 1, STAGE && PG_PRED, STAGE == 3, NOPAIR, EPWIN>(T, T.node, img, s1, d1, sp1, dp1, pr1, h, o);
         else classify_q<MODE, COUNT, 1, STAGE == 1 && PG_PRED>(T, blobs, tab0, s1, d1, sp1, dp1, pr1, h, o, rootb);
         out[i] = o[0];
     }
@@ -1096,7 +1102,20 @@ static void launch_classify(const DevTableSet& T, const Tuning& tu, int t, const
             if (nopair) return go1(std::integral_constant<int, S + 32>{}, Ts, words);
             go1(stage, Ts, words);
         };
-        if (T.node.cmap && (fits(all) || fits(norec))) {
+        // PERPOD without PAIR tables: the image staged whole with the end-point window after it
+        // (+ 64, k_classify EPWIN)
+        const bool epw = MODE == 1 && nopair && T.node.ep_span && PG_NODE_EPWIN;
+        const uint32_t ep_end =
+            T.node.ep_off + (uint32_t)(((uint64_t)T.node.ep_span * (T.node.ep_wide ? 2u : 1u) + 15u) / 16u * 4u);
+        auto go_ep = [&](auto stage, uint32_t words) {
+            constexpr int S = decltype(stage)::value;
+            if constexpr (MODE == 1) go1(std::integral_constant<int, S + 96>{}, T, words);
+        };
+        if (epw && T.node.cmap && fits(ep_end)) {
+            go_ep(std::integral_constant<int, 3>{}, ep_end);
+        } else if (epw && !T.node.cmap && ep_end <= tu.node_stage_max_words) {
+            go_ep(std::integral_constant<int, 1>{}, ep_end);
+        } else if (T.node.cmap && (fits(all) || fits(norec))) {
             const uint32_t w = fits(all) ? all : norec;
             if (w < all) Tn.node.lrec = 0;
             go(std::integral_constant<int, 3>{}, Tn, w);

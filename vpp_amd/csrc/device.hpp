@@ -90,7 +90,17 @@ struct DevNode {
     // (record word p of the cross numbering is image word p - rec0 + lrec); launches that do not
     // stage that part of the image clear lrec and read the cross array
     uint32_t rec0, lrec;
+    // PERPOD end-point window (ep_span != 0): for dst in [ep_base, ep_base + ep_span), the end
+    // point of dst as one u8 (ep_wide 0) or u16 (ep_wide 1) code at byte ep_off * 4 of the image
+    // (after everything above; staged by PERPOD launches only): the outbound table of a local
+    // pod, or kEpNode / kEpUnresolved / kEpNoAcl (device.hpp); any dst outside the window, and
+    // every pod of another node, is the node-output end point. PERPOD needs dst only for its
+    // end point when the node has no PAIR tables, so such launches skip dst's trie walk and its
+    // ipinfo read (one LDS byte read instead of ip_depth + 1 dependent reads).
+    uint32_t ep_base, ep_span, ep_off, ep_wide;
 };
+// end-point window codes (u8 codes are these & 0xFF)
+constexpr uint32_t kEpNode = 0xFFFFu, kEpUnresolved = 0xFFFEu, kEpNoAcl = 0xFFFDu;
 
 // table sets of up to this many counter slots are counted by a full LDS histogram (one cell per
 // slot, 64 KiB with the two extra cells of a SINGLE window)
@@ -173,6 +183,7 @@ struct Tuning {
     uint32_t node_hist_cells = 256;   // LDS slot-cache cells (rounded down to a power of two; < 16 = none)
                                       // of node launches whose set has more slots than the LDS histogram
     uint32_t node_list_words = 4096;  // node dst records up to this many words go into the image (0 = never)
+    uint32_t node_ep_window = 16384;  // PERPOD end-point window up to this many addresses (0 = none; DevNode)
     // launches
     uint32_t blocks_per_cu = 0;    // cap on resident workgroups per CU (0 = occupancy)
     uint32_t stage_max_words = kStageBlobWords;  // table blobs staged whole in LDS

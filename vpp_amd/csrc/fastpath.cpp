@@ -37,6 +37,7 @@
 //   fall-through verdict, a candidate list (CAND, CANDI) flags its last record instead (no
 //   match there: the table's default deny; an empty list is one match-all record carrying it).
 #include <algorithm>
+#include <cstring>
 #include <map>
 #include <set>
 #include <unordered_map>
@@ -890,6 +891,38 @@ void build_common_rows(HostTableSet& h, const std::vector<uint32_t>& cov, const 
     N.img_words = (uint32_t)img.size();
 }
 
+// PERPOD end-point window (DevNode ep_*): one code per address from the lowest to the highest
+// local pod address, appended after the image proper (img_words). Pods of another node and
+// every address outside the window take the node-output end point, like the trie's node class.
+static void build_ep_window(HostTableSet& h, const std::vector<NodePod>& ps, uint32_t T, const Tuning& tu) {
+    DevNode& N = h.node;
+    N.ep_base = N.ep_span = N.ep_off = N.ep_wide = 0;
+    auto local = [](const NodePod& p) { return p.ifc < 0 || ((uint32_t)p.ifc >> kEndKindShift) == 0; };
+    uint32_t lo = 0xFFFFFFFFu, hi = 0;
+    size_t n = 0;
+    for (const NodePod& p : ps)
+        if (local(p)) lo = std::min(lo, p.ip), hi = std::max(hi, p.ip), n++;
+    if (!n || tu.node_ep_window == 0 || (uint64_t)hi - lo + 1 > tu.node_ep_window || T >= kEpNoAcl) return;
+    const bool wide = T >= (kEpNoAcl & 0xFFu);
+    const uint32_t span = hi - lo + 1;
+    std::vector<uint8_t> bytes((size_t)span * (wide ? 2 : 1), 0xFF);  // kEpNode everywhere
+    for (const NodePod& p : ps) {
+        if (!local(p)) continue;
+        const uint32_t code = p.ifc < 0 ? kEpUnresolved : (p.tout < 0 ? kEpNoAcl : (uint32_t)p.tout);
+        const size_t o = p.ip - lo;
+        if (wide) bytes[2 * o] = code & 0xFFu, bytes[2 * o + 1] = code >> 8;
+        else bytes[o] = code & 0xFFu;
+    }
+    std::vector<uint32_t>& img = h.node_img;
+    while (img.size() % 4) img.push_back(0);
+    N.ep_off = (uint32_t)img.size();
+    img.resize(img.size() + (bytes.size() + 15) / 16 * 4, 0);
+    std::memcpy(img.data() + N.ep_off, bytes.data(), bytes.size());
+    N.ep_base = lo;
+    N.ep_span = span;
+    N.ep_wide = wide;
+}
+
 bool build_node(HostTableSet& h, const std::vector<TableAnalysis*>& an, const std::vector<NodePod>& pods,
                 const NodePod& node_end, const Tuning& tu) {
     h.node_img.clear();
@@ -1121,6 +1154,7 @@ bool build_node(HostTableSet& h, const std::vector<TableAnalysis*>& an, const st
         img.insert(img.end(), recs.begin(), recs.end());
         N.img_words = (uint32_t)img.size();
     }
+    build_ep_window(h, ps, T, tu);
     if (X.empty()) X.resize(4, 0);
     return true;
 }
