@@ -630,6 +630,7 @@ DevTableSet host_view(const HostTableSet& h) {
     v.node = h.node;
     v.node.img = h.node_img.empty() ? nullptr : h.node_img.data();
     v.node.cross = h.node_img.empty() ? nullptr : h.node_cross.data();
+    v.node.img_ep = h.node_img_ep.empty() ? nullptr : h.node_img_ep.data();
     v.host_tabs = h.tabs.data();
     v.host_blob_words = h.blob_words.data();
     v.host_blob_prefix = h.blob_prefix.data();
@@ -653,7 +654,9 @@ void host_q(const DevTableSet& T, bool node, int table_id, const pg_tuple_soa* t
             classify_q<0, true, Q, PRED>(T, T.blobs, tab, s, d, sp, dp, pr, h, o);
         }
     } else {
-        if (node) classify_node_q<MODE, true, Q, PRED, CM, false, EPW>(T, T.node, DevLoader{T.node.img}, s, d, sp, dp, pr, h, o);
+        if (node)  // (EPW: the image copy carrying the end-point window)
+            classify_node_q<MODE, true, Q, PRED, CM, false, EPW>(T, T.node, DevLoader{EPW ? T.node.img_ep : T.node.img}, s,
+                                                                 d, sp, dp, pr, h, o);
         else classify_q<MODE, true, Q, PRED>(T, T.blobs, DevTable{}, s, d, sp, dp, pr, h, o);
     }
     for (int j = 0; j < Q; j++) out[i + j] = o[j];
@@ -693,7 +696,7 @@ int pg_debug_classify_host(pg_ctx* ctx, int mode, int table_id, const pg_tuple_s
     const bool use_node = (node & 1) && T.node.img != nullptr, pred = (node & 2) != 0;
     const bool cm = use_node && (node & 4) && T.node.cmap != 0;
     // the PERPOD end-point window, where the kernels use it (a node without PAIR tables)
-    const bool epw = use_node && (node & 8) && T.node.ep_span != 0 && T.node.n_pair == 0;
+    const bool epw = use_node && (node & 8) && T.node.img_ep != nullptr && T.node.n_pair == 0;
     const Hist h{nullptr, (unsigned long long*)counters};
     if (mode == 0) host_classify<0, false>(T, false, pred, false, table_id, t, n, out, h);
     else if (mode == 1 && epw) host_classify<1, true>(T, use_node, pred, cm, table_id, t, n, out, h);

@@ -169,6 +169,7 @@ DeviceBuffers* dev_upload(const HostTableSet& h, std::string* err) {
     size_t o_ip = place(h.iphash.size() * 4);
     size_t o_nimg = place(h.node_img.size() * 4);
     size_t o_nx = place(h.node_cross.size() * 4);
+    size_t o_nep = place(h.node_img_ep.size() * 4);
     std::vector<uint8_t> img(off, 0);
     auto put = [&](size_t o, const void* p, size_t n) {
         if (n) std::memcpy(img.data() + o, p, n);
@@ -180,6 +181,7 @@ DeviceBuffers* dev_upload(const HostTableSet& h, std::string* err) {
     put(o_ip, h.iphash.data(), h.iphash.size() * 4);
     put(o_nimg, h.node_img.data(), h.node_img.size() * 4);
     put(o_nx, h.node_cross.data(), h.node_cross.size() * 4);
+    put(o_nep, h.node_img_ep.data(), h.node_img_ep.size() * 4);
     auto* b = new DeviceBuffers();
     b->blob = dev_alloc(off, err);
     if (!b->blob) {
@@ -212,6 +214,7 @@ DeviceBuffers* dev_upload(const HostTableSet& h, std::string* err) {
     v.node = h.node;
     v.node.img = h.node_img.empty() ? nullptr : (const uint32_t*)(base + o_nimg);
     v.node.cross = h.node_img.empty() ? nullptr : (const uint32_t*)(base + o_nx);
+    v.node.img_ep = h.node_img_ep.empty() ? nullptr : (const uint32_t*)(base + o_nep);
     b->host_tabs = h.tabs;
     b->host_blob_words = h.blob_words;
     b->host_blob_prefix = h.blob_prefix;
@@ -1102,19 +1105,22 @@ static void launch_classify(const DevTableSet& T, const Tuning& tu, int t, const
             if (nopair) return go1(std::integral_constant<int, S + 32>{}, Ts, words);
             go1(stage, Ts, words);
         };
-        // PERPOD without PAIR tables: the image staged whole with the end-point window after it
-        // (+ 64, k_classify EPWIN)
-        const bool epw = MODE == 1 && nopair && T.node.ep_span && PG_NODE_EPWIN;
-        const uint32_t ep_end =
-            T.node.ep_off + (uint32_t)(((uint64_t)T.node.ep_span * (T.node.ep_wide ? 2u : 1u) + 15u) / 16u * 4u);
+        // PERPOD without PAIR tables: the image copy with the end-point window (img_ep; + 64,
+        // k_classify EPWIN), staged like the image itself when the window sits over ipinfo
+        // (records left out when only that fits), else only when all of it fits
+        const bool epw = MODE == 1 && nopair && T.node.img_ep && PG_NODE_EPWIN;
+        const bool ep_in = T.node.ep_img_words == all;  // the window over ipinfo
+        DevTableSet Te = T;
+        Te.node.img = T.node.img_ep;
         auto go_ep = [&](auto stage, uint32_t words) {
             constexpr int S = decltype(stage)::value;
-            if constexpr (MODE == 1) go1(std::integral_constant<int, S + 96>{}, T, words);
+            if (words < T.node.ep_img_words) Te.node.lrec = 0;  // (in place: the records left out)
+            if constexpr (MODE == 1) go1(std::integral_constant<int, S + 96>{}, Te, words);
         };
-        if (epw && T.node.cmap && fits(ep_end)) {
-            go_ep(std::integral_constant<int, 3>{}, ep_end);
-        } else if (epw && !T.node.cmap && ep_end <= tu.node_stage_max_words) {
-            go_ep(std::integral_constant<int, 1>{}, ep_end);
+        if (epw && T.node.cmap && (fits(T.node.ep_img_words) || (ep_in && fits(norec)))) {
+            go_ep(std::integral_constant<int, 3>{}, fits(T.node.ep_img_words) ? T.node.ep_img_words : norec);
+        } else if (epw && !T.node.cmap && T.node.ep_img_words <= tu.node_stage_max_words) {
+            go_ep(std::integral_constant<int, 1>{}, T.node.ep_img_words);
         } else if (T.node.cmap && (fits(all) || fits(norec))) {
             const uint32_t w = fits(all) ? all : norec;
             if (w < all) Tn.node.lrec = 0;

@@ -91,13 +91,16 @@ struct DevNode {
     // stage that part of the image clear lrec and read the cross array
     uint32_t rec0, lrec;
     // PERPOD end-point window (ep_span != 0): for dst in [ep_base, ep_base + ep_span), the end
-    // point of dst as one u8 (ep_wide 0) or u16 (ep_wide 1) code at byte ep_off * 4 of the image
-    // (after everything above; staged by PERPOD launches only): the outbound table of a local
-    // pod, or kEpNode / kEpUnresolved / kEpNoAcl (device.hpp); any dst outside the window, and
-    // every pod of another node, is the node-output end point. PERPOD needs dst only for its
-    // end point when the node has no PAIR tables, so such launches skip dst's trie walk and its
-    // ipinfo read (one LDS byte read instead of ip_depth + 1 dependent reads).
-    uint32_t ep_base, ep_span, ep_off, ep_wide;
+    // point of dst as one u8 (ep_wide 0) or u16 (ep_wide 1) code at byte ep_off * 4 of img_ep:
+    // the outbound table of a local pod, or kEpNode / kEpUnresolved / kEpNoAcl; any dst outside
+    // the window, and every pod of another node, is the node-output end point. PERPOD needs dst
+    // only for its end point when the node has no PAIR tables, so such launches skip dst's trie
+    // walk and its ipinfo read (one LDS byte read instead of ip_depth + 1 dependent reads).
+    // img_ep is a copy of img with the window written over ipinfo (which such launches never
+    // read), so staging it takes no more LDS than img; when the window is larger than ipinfo it
+    // is appended instead (ep_img_words > img_words: staged only when everything fits).
+    const uint32_t* img_ep;
+    uint32_t ep_base, ep_span, ep_off, ep_wide, ep_img_words;
 };
 // end-point window codes (u8 codes are these & 0xFF)
 constexpr uint32_t kEpNode = 0xFFFFu, kEpUnresolved = 0xFFFEu, kEpNoAcl = 0xFFFDu;
@@ -155,6 +158,7 @@ struct HostTableSet {
     int32_t node_if = -1, node_in = -1, node_out = -1;
     uint32_t slot_hot_in = 0xFFFFFFFFu;          // DevTableSet.slot_hot_in (engine.cpp compile)
     std::vector<uint32_t> node_img, node_cross;  // empty img: no node classifier
+    std::vector<uint32_t> node_img_ep;           // DevNode img_ep (empty: no end-point window)
     DevNode node{};                              // header fields (pointers unset)
     uint32_t node_rec_words = 0;                 // words of the node's dst records (build_node)
 };

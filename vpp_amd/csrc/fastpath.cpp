@@ -892,11 +892,14 @@ void build_common_rows(HostTableSet& h, const std::vector<uint32_t>& cov, const 
 }
 
 // PERPOD end-point window (DevNode ep_*): one code per address from the lowest to the highest
-// local pod address, appended after the image proper (img_words). Pods of another node and
-// every address outside the window take the node-output end point, like the trie's node class.
+// local pod address, in a copy of the image (img_ep) over its ipinfo section when it fits there
+// (PERPOD launches that use the window never read ipinfo), else appended to that copy. Pods of
+// another node and every address outside the window take the node-output end point, like the
+// trie's node class.
 static void build_ep_window(HostTableSet& h, const std::vector<NodePod>& ps, uint32_t T, const Tuning& tu) {
     DevNode& N = h.node;
-    N.ep_base = N.ep_span = N.ep_off = N.ep_wide = 0;
+    N.ep_base = N.ep_span = N.ep_off = N.ep_wide = N.ep_img_words = 0;
+    h.node_img_ep.clear();
     auto local = [](const NodePod& p) { return p.ifc < 0 || ((uint32_t)p.ifc >> kEndKindShift) == 0; };
     uint32_t lo = 0xFFFFFFFFu, hi = 0;
     size_t n = 0;
@@ -913,11 +916,17 @@ static void build_ep_window(HostTableSet& h, const std::vector<NodePod>& ps, uin
         if (wide) bytes[2 * o] = code & 0xFFu, bytes[2 * o + 1] = code >> 8;
         else bytes[o] = code & 0xFFu;
     }
-    std::vector<uint32_t>& img = h.node_img;
-    while (img.size() % 4) img.push_back(0);
-    N.ep_off = (uint32_t)img.size();
-    img.resize(img.size() + (bytes.size() + 15) / 16 * 4, 0);
+    std::vector<uint32_t>& img = h.node_img_ep;
+    img = h.node_img;
+    if (bytes.size() <= (size_t)N.n_ipc * 8u) {  // over ipinfo (uint2 per IP class)
+        N.ep_off = N.ipinfo;
+    } else {
+        while (img.size() % 4) img.push_back(0);
+        N.ep_off = (uint32_t)img.size();
+        img.resize(img.size() + (bytes.size() + 15) / 16 * 4, 0);
+    }
     std::memcpy(img.data() + N.ep_off, bytes.data(), bytes.size());
+    N.ep_img_words = (uint32_t)img.size();
     N.ep_base = lo;
     N.ep_span = span;
     N.ep_wide = wide;
@@ -928,6 +937,7 @@ bool build_node(HostTableSet& h, const std::vector<TableAnalysis*>& an, const st
     h.node_img.clear();
     h.node_cross.clear();
     h.node = DevNode{};
+    h.node_img_ep.clear();
     h.node_rec_words = 0;
     const uint32_t T = (uint32_t)h.tabs.size();
     if (!tu.node_build || T == 0 || T >= 0xFFFFu) return false;
