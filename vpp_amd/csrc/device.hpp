@@ -182,6 +182,7 @@ struct Tuning {
     uint32_t node_root_bits = 12;  // its IPv4 / key trie root stride cap (4..16)
     uint32_t node_common = 1;      // common-row section of node images
     uint32_t fd = 1;               // FD form of dst-independent CROSS tables that fit LDS
+    uint32_t fd_l2_words = 0;      // FD blobs read from HBM: prefer a trie shape within this many words (0 = fewest levels)
     uint32_t candi = 1;            // CANDI form (inline candidates) of dst-independent HBM-resident CAND tables
     uint32_t cross_max_rules = 1u << 20;  // CROSS (cross product) considered up to this many rules (within budget)
     uint32_t node_hist_cells = 256;   // LDS slot-cache cells (rounded down to a power of two; < 16 = none)

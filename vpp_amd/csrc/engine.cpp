@@ -52,6 +52,7 @@ const Knob kKnobs[] = {
     {"node_root_bits", &Tuning::node_root_bits, 4, 16, true},
     {"node_common", &Tuning::node_common, 0, 1, true},
     {"fd", &Tuning::fd, 0, 1, true},
+    {"fd_l2_words", &Tuning::fd_l2_words, 0, 1 << 22, true},
     {"candi", &Tuning::candi, 0, 1, true},
     {"cross_max_rules", &Tuning::cross_max_rules, 0, 1 << 24, true},
     {"node_hist_cells", &Tuning::node_hist_cells, 0, 8192, false},

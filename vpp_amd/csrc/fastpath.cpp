@@ -825,7 +825,11 @@ bool build_fd_blob(const TableAnalysis& A, uint32_t dflt, const Tuning& tu, std:
         blob[9] = (P + K + 3u) & ~3u;
         blob[10] = A.nsc;
         if (blob.size() <= lds_words) return true;
-        if (best.empty()) best.swap(blob);
+        // read from HBM: the fewest levels, unless Tuning::fd_l2_words asks for a blob an XCD's
+        // L2 holds -- then the first shape within it, or else the smallest
+        const bool l2 = tu.fd_l2_words != 0;
+        if (best.empty() || (l2 && best.size() > tu.fd_l2_words && blob.size() < best.size())) best.swap(blob);
+        if (l2 && best.size() <= tu.fd_l2_words) break;
     }
     if (best.empty()) return false;
     blob.swap(best);
