@@ -304,7 +304,9 @@ PG_HD void blob_walk(const L (&ld)[Q], const BlobTab (&tb)[Q], const bool (&on)[
 // word and every lookup takes the same D reads: src -> the self word heading its src class's
 // verdict row, key -> the self word of its key class. Verdict = the word at (src self) +
 // (key self) + bias, i.e. row[1 + key class]. fsk: s1 << 8 | k1 << 16; kroot: key trie root;
-// depth: reads per field; bias: 1 - (first key self word).
+// depth: reads of the src walk | reads of the key walk << 8 (each walk takes its own trie's
+// depth: a shallow key trie does not re-read its self words for the src trie's extra levels);
+// bias: 1 - (first key self word).
 // lp reads the blob's prefix (header, src root, key trie and self words: the LDS copy when a
 // launch stages only that), lb everything else (the src levels below the root and the rows).
 PG_HD uint32_t fd_child(uint32_t e, uint32_t a) {
@@ -318,6 +320,9 @@ PG_HD uint32_t fd_child(uint32_t e, uint32_t a) {
 // SKIP (the src levels in HBM / L2): a lane whose src entry is already a self word (stride 0)
 // does not re-read it -- an exec-masked gather costs the texture path nothing for that lane, and
 // large FD tables are bound by that path (profiles/r03_v2_config7_util.json: TA busy 0.93)
+#ifndef PG_FD_SPLIT  // each FD walk takes its own trie's depth
+#define PG_FD_SPLIT 1
+#endif
 template <bool SKIP = false, class LP, class LB, int Q>
 PG_HD void fd_walk(const LP& lp, const LB& lb, uint32_t fsk, uint32_t kroot, uint32_t depth, uint32_t bias,
                    const uint32_t (&src)[Q], const uint32_t (&key)[Q], uint32_t (&w)[Q]) {
@@ -328,12 +333,26 @@ PG_HD void fd_walk(const LP& lp, const LB& lb, uint32_t fsk, uint32_t kroot, uin
         es[j] = lp.u32(kSrcRoot + (src[j] >> ss));
         ek[j] = lp.u32(kroot + (key[j] >> sk));
     }
-    for (uint32_t l = 1; l < depth; l++) {
+#if PG_FD_SPLIT
+    const uint32_t ds = depth & 0xFFu, dk = depth >> 8, dmin = ds < dk ? ds : dk;
+#else  // A/B build: both walks take the deeper trie's depth
+    const uint32_t ds = (depth & 0xFFu) > (depth >> 8) ? depth & 0xFFu : depth >> 8, dk = ds, dmin = ds;
+#endif
+    for (uint32_t l = 1; l < dmin; l++) {  // both walks in lockstep (independent reads overlap)
         PG_UNROLL
         for (int j = 0; j < Q; j++) {
             if (!SKIP || (es[j] & 0x3E0u)) es[j] = lb.u32(fd_child(es[j], src[j]));
             ek[j] = lp.u32(fd_child(ek[j], key[j]));
         }
+    }
+    for (uint32_t l = dmin; l < ds; l++) {
+        PG_UNROLL
+        for (int j = 0; j < Q; j++)
+            if (!SKIP || (es[j] & 0x3E0u)) es[j] = lb.u32(fd_child(es[j], src[j]));
+    }
+    for (uint32_t l = dmin; l < dk; l++) {
+        PG_UNROLL
+        for (int j = 0; j < Q; j++) ek[j] = lp.u32(fd_child(ek[j], key[j]));
     }
     PG_UNROLL
     for (int j = 0; j < Q; j++) w[j] = lb.u32((es[j] >> 10) + (ek[j] >> 10) + bias);

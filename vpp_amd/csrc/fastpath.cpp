@@ -819,7 +819,7 @@ bool build_fd_blob(const TableAnalysis& A, uint32_t dflt, const Tuning& tu, std:
         blob[3] = s1;
         blob[4] = P;
         blob[5] = k1;
-        blob[6] = std::max(ds, dk);
+        blob[6] = ds | dk << 8;  // reads per walk (fd_walk)
         blob[7] = 1u - kself;
         blob[8] = A.nkc;
         blob[9] = (P + K + 3u) & ~3u;
