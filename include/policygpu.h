@@ -169,10 +169,7 @@ int pg_ctx_device(const pg_ctx* ctx);
  * cross-product tables, default 1), "node_common" (1/0: common-row section of node
  * images, default 1), "node_list_words" (node dst records -- the dst-specific rules a node
  * cross entry must still test -- up to this many words go into the node image, so a launch that
- * stages the image walks them in LDS; default 4096, 0 = never), "node_ep_window" (PERPOD
- * end-point window: one code per address between the lowest and highest local pod address, up to
- * this many addresses, so PERPOD launches over a node without PAIR tables resolve dst's end
- * point with one LDS read instead of its trie walk; default 16384, 0 = never), "pair" (1/0: the PAIR structure -- src x dst classes, then x key classes
+ * stages the image walks them in LDS; default 4096, 0 = never), "pair" (1/0: the PAIR structure -- src x dst classes, then x key classes
  * -- for tables the cross product cannot take, default 1; 0 = candidate lists; 2 = wherever it
  * fits, for tests).
  * pg_ctx_set_tuning sets one context's knob; pg_set_tuning sets the process default that
@@ -245,9 +242,7 @@ int pg_debug_walk_blob(pg_ctx* ctx, const char* acl_name, const uint32_t* src, c
  * optional host u64 counters. flags: bit 0 = node classifier when it exists (else the
  * per-table path), bit 1 = the predicated trie walks the kernels use on LDS-staged images
  * (else the branching ones they use on HBM-resident ones), bit 2 = the node image's
- * common-row section when it was built (the kernels use it when it fits their LDS budget), bit 3 =
- * PERPOD: dst's end point from the node's end-point window when it was built (tuning
- * "node_ep_window"; node sets without PAIR tables, as the kernels do).
+ * common-row section when it was built (the kernels use it when it fits their LDS budget).
  * Does not touch the device. */
 int pg_debug_classify_host(pg_ctx* ctx, int mode, int table_id, const pg_tuple_soa* tuples, uint64_t n,
                            uint32_t* out, uint64_t* counters, int flags);
@@ -274,9 +269,6 @@ int pg_node_common_stats(pg_ctx* ctx, uint64_t* base_image_bytes, uint64_t* comm
 /* the node classifier's dst records (the dst-specific rules its cross entries still test): their
  * bytes, and whether a copy ends the node image (tuning "node_list_words"); PG_ENOENT: no node */
 int pg_node_list_stats(pg_ctx* ctx, uint64_t* record_bytes, int* in_image);
-/* the node's PERPOD end-point window (tuning "node_ep_window"): first address, addresses
- * (0 = not built), 1 = u16 codes (else u8); PG_ENOENT: no node */
-int pg_node_ep_stats(pg_ctx* ctx, uint32_t* base, uint32_t* span, int* wide);
 /* reference-shaped linear-scan kernel (K1) on one table, for validation and comparison */
 int pg_classify_linear(pg_ctx* ctx, int table_id, const pg_tuple_soa* tuples, uint64_t n, uint32_t* out,
                        void* hip_stream);

@@ -83,11 +83,6 @@ def check(e, local, tup, expect_node=True):
     # fit their LDS budget): same verdicts and counters
     p0, c0 = e.debug_classify_host(MODE_PERPOD, -1, *tup, counters=True, node=True, common=False)
     assert np.array_equal(p0, pn) and np.array_equal(c0, cpn)
-    # PERPOD with dst's end point from the end-point window (nodes without PAIR tables; the
-    # flag is ignored otherwise): same verdicts and counters, with and without common rows
-    for cm in (True, False):
-        pe, ce = e.debug_classify_host(MODE_PERPOD, -1, *tup, counters=True, node=True, common=cm, epwin=True)
-        assert np.array_equal(pe, pn) and np.array_equal(ce, cpn)
     q0, d0 = e.debug_classify_host(MODE_CONN, -1, *tup, counters=True, node=True, common=False)
     q1, d1 = e.debug_classify_host(MODE_CONN, -1, *tup, counters=True, node=True)
     assert np.array_equal(q0, q1) and np.array_equal(d0, d1)
@@ -184,11 +179,6 @@ def test_config3_cluster_node_path():
     assert np.array_equal(got >> 30, conn.astype(np.uint32)) and np.array_equal(got & 0x3FFFFFFF, cslot)
     got0 = e.debug_classify_host(MODE_CONN, -1, src, dst, sport, dport, proto, node=True, common=False)
     assert np.array_equal(got0, got)
-    # the PERPOD end-point window: every local pod between 10.1.0.1 and 10.1.9.90, u8 codes
-    assert ns["ep_window_addresses"] == (9 << 8) + 90 and not ns["ep_window_wide"], ns
-    assert ns["ep_window_base"] == W.ip_u32("10.1.0.1"), ns
-    got = e.debug_classify_host(MODE_PERPOD, -1, src, dst, sport, dport, proto, node=True, epwin=True)
-    assert np.array_equal(got >> 30, act.astype(np.uint32)) and np.array_equal(got & 0x3FFFFFFF, slot)
     # the global table's dst-specific rules: dst records, a copy at the end of the image
     assert ns["list_record_bytes"] > 0 and ns["list_records_in_image"], ns
 
@@ -273,36 +263,3 @@ def test_config6_pair_table_covered():
     act, slot = wd.perpod(src, dst, dport, proto, threads=8)
     got = e.debug_classify_host(MODE_PERPOD, -1, src, dst, sport, dport, proto, node=True)
     assert np.array_equal(got >> 30, act.astype(np.uint32)) and np.array_equal(got & 0x3FFFFFFF, slot)
-
-
-def test_ep_window_appended_when_larger_than_ipinfo():
-    """Two local pods far apart and few node IP classes: the end-point window (7.7k addresses)
-    does not fit over ipinfo and is appended to the image copy; PERPOD through it equals the
-    trie walk and the oracle. With node_ep_window below the span there is no window."""
-    e = R.Engine(0)
-    e.SetVxlanBVIIfName("VXLAN-BVI")
-    pods = {"ns/a": ("10.0.0.1", "tapA"), "ns/b": ("10.0.30.1", "tapB"), "ns/c": ("10.0.15.7", None)}
-    for p, (ip, ifn) in pods.items():
-        if ifn:
-            e.SetPodIfName(p, ifn)
-        e.RegisterPod(p, ip, False)
-    e.RegisterPod("ns/r", "10.0.20.2", True)
-    e.ApplyTxn(True, [("config/vpp/acls/v2/acl/o", {"name": "o", "rules": [{"action": 1, "src": "10.0.0.0/16", "dst": "",
-                                                                            "tcp": {"src": [0, 65535], "dst": [80, 80]}}],
-                                                    "ingress": [], "egress": ["tapA"]}),
-                      ("config/vpp/acls/v2/acl/g", {"name": "g", "rules": [{"action": 0, "src": "10.0.0.1/32", "dst": ""}],
-                                                    "ingress": [], "egress": ["VXLAN-BVI"]})])
-    ns = e.node_stats()
-    assert ns["ep_window_addresses"] == 30 * 256 + 1 and ns["ip_classes"] * 8 < ns["ep_window_addresses"], ns
-    ips = [W.ip_u32(x) for x, _ in pods.values()] + [W.ip_u32("10.0.20.2"), W.ip_u32("8.8.8.8")]
-    tup = tuples(11, 5003, ips)
-    pn, cpn = e.debug_classify_host(MODE_PERPOD, -1, *tup, counters=True, node=True)
-    pe, cpe = e.debug_classify_host(MODE_PERPOD, -1, *tup, counters=True, node=True, epwin=True)
-    assert np.array_equal(pe, pn) and np.array_equal(cpe, cpn)
-    wd = World(e, {W.ip_u32("10.0.0.1"): "tapA", W.ip_u32("10.0.30.1"): "tapB"}, "VXLAN-BVI",
-               no_if_ips=[W.ip_u32("10.0.15.7")])
-    act, slot = wd.perpod(*tup[:2], tup[3], tup[4])
-    assert np.array_equal(pe >> 30, act.astype(np.uint32)) and np.array_equal(pe & 0x3FFFFFFF, slot)
-    assert {3, 1, 0} <= set((pe >> 30).tolist())  # unresolved pod, permits, denies
-    with e.tuning(node_ep_window=1000):
-        assert e.node_stats()["ep_window_addresses"] == 0

@@ -167,7 +167,6 @@ _SIGS = {
                                 C.POINTER(C.c_uint64)]),
     "pg_node_common_stats": (C.c_int, [_P, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
     "pg_node_list_stats": (C.c_int, [_P, C.POINTER(C.c_uint64), C.POINTER(C.c_int)]),
-    "pg_node_ep_stats": (C.c_int, [_P, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.POINTER(C.c_int)]),
     "pg_configurator_new": (_P, []),
     "pg_configurator_free": (None, [_P]),
     "pg_configurator_last_error": (C.c_char_p, [_P]),

@@ -345,6 +345,11 @@ PG_HD void fd_walk(const LP& lp, const LB& lb, uint32_t fsk, uint32_t kroot, uin
             ek[j] = lp.u32(fd_child(ek[j], key[j]));
         }
     }
+    if (ds == dk) {  // (uniform) equal depths, the compiler's default: no further loop control
+        PG_UNROLL
+        for (int j = 0; j < Q; j++) w[j] = lb.u32((es[j] >> 10) + (ek[j] >> 10) + bias);
+        return;
+    }
     for (uint32_t l = dmin; l < ds; l++) {
         PG_UNROLL
         for (int j = 0; j < Q; j++)

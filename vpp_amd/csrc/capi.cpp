@@ -630,14 +630,13 @@ DevTableSet host_view(const HostTableSet& h) {
     v.node = h.node;
     v.node.img = h.node_img.empty() ? nullptr : h.node_img.data();
     v.node.cross = h.node_img.empty() ? nullptr : h.node_cross.data();
-    v.node.img_ep = h.node_img_ep.empty() ? nullptr : h.node_img_ep.data();
     v.host_tabs = h.tabs.data();
     v.host_blob_words = h.blob_words.data();
     v.host_blob_prefix = h.blob_prefix.data();
     return v;
 }
 
-template <int MODE, int Q, bool PRED, bool CM, bool EPW>
+template <int MODE, int Q, bool PRED, bool CM>
 void host_q(const DevTableSet& T, bool node, int table_id, const pg_tuple_soa* t, uint64_t i, uint32_t* out,
             const Hist& h) {
     uint32_t s[Q], d[Q], sp[Q], dp[Q], pr[Q], o[Q];
@@ -654,28 +653,26 @@ void host_q(const DevTableSet& T, bool node, int table_id, const pg_tuple_soa* t
             classify_q<0, true, Q, PRED>(T, T.blobs, tab, s, d, sp, dp, pr, h, o);
         }
     } else {
-        if (node)  // (EPW: the image copy carrying the end-point window)
-            classify_node_q<MODE, true, Q, PRED, CM, false, EPW>(T, T.node, DevLoader{EPW ? T.node.img_ep : T.node.img}, s,
-                                                                 d, sp, dp, pr, h, o);
+        if (node) classify_node_q<MODE, true, Q, PRED, CM>(T, T.node, DevLoader{T.node.img}, s, d, sp, dp, pr, h, o);
         else classify_q<MODE, true, Q, PRED>(T, T.blobs, DevTable{}, s, d, sp, dp, pr, h, o);
     }
     for (int j = 0; j < Q; j++) out[i + j] = o[j];
 }
 
-template <int MODE, bool PRED, bool CM, bool EPW>
+template <int MODE, bool PRED, bool CM>
 void host_classify(const DevTableSet& T, bool node, int table_id, const pg_tuple_soa* t, uint64_t n, uint32_t* out,
                    const Hist& h) {
     const uint64_t nq = n & ~(uint64_t)3;  // the kernels' quads, then one tuple at a time
-    for (uint64_t i = 0; i < nq; i += 4) host_q<MODE, 4, PRED, CM, EPW>(T, node, table_id, t, i, out, h);
-    for (uint64_t i = nq; i < n; i++) host_q<MODE, 1, PRED, CM, EPW>(T, node, table_id, t, i, out, h);
+    for (uint64_t i = 0; i < nq; i += 4) host_q<MODE, 4, PRED, CM>(T, node, table_id, t, i, out, h);
+    for (uint64_t i = nq; i < n; i++) host_q<MODE, 1, PRED, CM>(T, node, table_id, t, i, out, h);
 }
-template <int MODE, bool EPW>
+template <int MODE>
 void host_classify(const DevTableSet& T, bool node, bool pred, bool cm, int table_id, const pg_tuple_soa* t,
                    uint64_t n, uint32_t* out, const Hist& h) {
-    if (pred && cm) host_classify<MODE, true, true, EPW>(T, node, table_id, t, n, out, h);
-    else if (pred) host_classify<MODE, true, false, EPW>(T, node, table_id, t, n, out, h);
-    else if (cm) host_classify<MODE, false, true, EPW>(T, node, table_id, t, n, out, h);
-    else host_classify<MODE, false, false, EPW>(T, node, table_id, t, n, out, h);
+    if (pred && cm) host_classify<MODE, true, true>(T, node, table_id, t, n, out, h);
+    else if (pred) host_classify<MODE, true, false>(T, node, table_id, t, n, out, h);
+    else if (cm) host_classify<MODE, false, true>(T, node, table_id, t, n, out, h);
+    else host_classify<MODE, false, false>(T, node, table_id, t, n, out, h);
 }
 }  // namespace
 
@@ -695,13 +692,10 @@ int pg_debug_classify_host(pg_ctx* ctx, int mode, int table_id, const pg_tuple_s
         return fail(ctx, PG_EINVAL, "missing tuple field");
     const bool use_node = (node & 1) && T.node.img != nullptr, pred = (node & 2) != 0;
     const bool cm = use_node && (node & 4) && T.node.cmap != 0;
-    // the PERPOD end-point window, where the kernels use it (a node without PAIR tables)
-    const bool epw = use_node && (node & 8) && T.node.img_ep != nullptr && T.node.n_pair == 0;
     const Hist h{nullptr, (unsigned long long*)counters};
-    if (mode == 0) host_classify<0, false>(T, false, pred, false, table_id, t, n, out, h);
-    else if (mode == 1 && epw) host_classify<1, true>(T, use_node, pred, cm, table_id, t, n, out, h);
-    else if (mode == 1) host_classify<1, false>(T, use_node, pred, cm, table_id, t, n, out, h);
-    else host_classify<2, false>(T, use_node, pred, cm, table_id, t, n, out, h);
+    if (mode == 0) host_classify<0>(T, false, pred, false, table_id, t, n, out, h);
+    else if (mode == 1) host_classify<1>(T, use_node, pred, cm, table_id, t, n, out, h);
+    else host_classify<2>(T, use_node, pred, cm, table_id, t, n, out, h);
     return PG_OK;
     GUARD_END(ctx)
 }
@@ -764,20 +758,6 @@ int pg_node_list_stats(pg_ctx* ctx, uint64_t* record_bytes, int* in_image) {
     if (h.node_img.empty()) return fail(ctx, PG_ENOENT, "no node classifier (disabled or over budget)");
     if (record_bytes) *record_bytes = (uint64_t)h.node_rec_words * 4;
     if (in_image) *in_image = h.node.lrec != 0;
-    return PG_OK;
-    GUARD_END(ctx)
-}
-
-int pg_node_ep_stats(pg_ctx* ctx, uint32_t* base, uint32_t* span, int* wide) {
-    if (!ctx) return PG_EINVAL;
-    GUARD_BEGIN
-    Engine& E = ctx->eng;
-    if (!E.compiled) E.compile();
-    const HostTableSet& h = E.host;
-    if (h.node_img.empty()) return fail(ctx, PG_ENOENT, "no node classifier (disabled or over budget)");
-    if (base) *base = h.node.ep_base;
-    if (span) *span = h.node.ep_span;
-    if (wide) *wide = (int)h.node.ep_wide;
     return PG_OK;
     GUARD_END(ctx)
 }

@@ -80,7 +80,6 @@ struct DevLoader {
         return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(b) + off);
     }
     PG_HD uint32_t u16(uint32_t i) const { return reinterpret_cast<const uint16_t*>(b)[i]; }  // halfword i
-    PG_HD uint32_t u8(uint32_t i) const { return reinterpret_cast<const uint8_t*>(b)[i]; }    // byte i
     PG_HD W2 u2(uint32_t i) const {
 #if defined(__HIP_DEVICE_COMPILE__)
         const uint2 v = *reinterpret_cast<const uint2*>(b + i);
@@ -111,7 +110,6 @@ struct LdsLoader {
     PG_HD uint32_t u32(uint32_t i) const { return at<uint32_t>(i * 4u); }
     PG_HD uint32_t at_byte(uint32_t off) const { return at<uint32_t>(off); }
     PG_HD uint32_t u16(uint32_t i) const { return at<uint16_t>(i * 2u); }
-    PG_HD uint32_t u8(uint32_t i) const { return at<uint8_t>(i); }
     PG_HD W2 u2(uint32_t i) const {
         const uint2 v = at<uint2>(i * 4u);
         return W2{v.x, v.y};
@@ -124,7 +122,6 @@ struct LdsLoader {
     uint32_t u32(uint32_t) const { return 0; }
     uint32_t at_byte(uint32_t) const { return 0; }
     uint32_t u16(uint32_t) const { return 0; }
-    uint32_t u8(uint32_t) const { return 0; }
     W2 u2(uint32_t) const { return W2{0, 0}; }
     W4 u4(uint32_t) const { return W4{0, 0, 0, 0}; }
 #endif
@@ -918,49 +915,14 @@ PG_HD void classify_q(const DevTableSet& T, const uint32_t* blobs, const DevTabl
 
 // Q tuples of one lane, PERPOD / CONN, node path. `img` reads the node image (LDS copy or
 // global memory).
-template <int MODE, bool COUNT, int Q, bool PRED = false, bool CM = false, bool NP = false, bool EPW = false,
-          class L, class HS, class H = NoHook>
+template <int MODE, bool COUNT, int Q, bool PRED = false, bool CM = false, bool NP = false, class L, class HS,
+          class H = NoHook>
 PG_HD void classify_node_q(const DevTableSet& T, const DevNode& N, const L& img, const uint32_t (&s)[Q],
                            const uint32_t (&d)[Q], const uint32_t (&sp)[Q], const uint32_t (&dp)[Q],
                            const uint32_t (&pr)[Q], const HS& h, uint32_t (&out)[Q], const H& hook = H()) {
     uint32_t key[Q], kack[Q];
     PG_UNROLL
     for (int j = 0; j < Q; j++) key[j] = pkt_key(pr[j], dp[j]), kack[j] = MODE == 2 ? pkt_key(pr[j], sp[j]) : key[j];
-    if constexpr (MODE == 1 && EPW) {
-        // PERPOD over a node without PAIR tables, with its end-point window (DevNode ep_*): dst
-        // is needed only for its end point, so only src and the key are walked; dst's outbound
-        // table is one code read from the window (u8 codes >= 0xFD stand for the u16 kEp* ones)
-        uint32_t keys[Q], cs[Q], gs[Q];
-        PG_UNROLL
-        for (int j = 0; j < Q; j++) keys[j] = key[j] < kWalkKeyLimit ? key[j] : 0u;
-        node_trie2_q<PRED>(img, N, s, cs, keys, gs);
-        int32_t t[Q];
-        bool run[Q];
-        PG_UNROLL
-        for (int j = 0; j < Q; j++) {
-            const uint32_t off = d[j] - N.ep_base;
-            const bool in = off < N.ep_span;
-            uint32_t code;
-            if (N.ep_wide) {
-                code = img.u16(2u * N.ep_off + (in ? off : 0u));
-            } else {
-                code = img.u8(4u * N.ep_off + (in ? off : 0u));
-                code = code >= (kEpNoAcl & 0xFFu) ? code | 0xFF00u : code;
-            }
-            code = in ? code : kEpNode;
-            run[j] = code == kEpNode ? T.node_if >= 0 : code != kEpUnresolved;
-            t[j] = code == kEpNode ? T.node_out : (code == kEpNoAcl ? -1 : (int32_t)code);
-            if (!run[j]) {
-                out[j] = verdict(kActFailure, T.slot_unresolved);
-                if (COUNT) h.inc_cold(T.slot_unresolved);
-            }
-        }
-        bool hooked = false;
-        const NodeEval<L, Q, H, CM, NP> ev{T, N, img, s, d, key, key, cs, cs, gs, gs, hook, &hooked};
-        eval_step<Q, COUNT>(T, ev, t, run, false, h, out);
-        if (!hooked) hook();  // no evaluation ran in this lane
-        return;
-    }
     // node IP classes of src and dst, node key classes of both keys: 2Q + 2Q trie walks
     uint32_t ips[2 * Q], ipc[2 * Q];
     PG_UNROLL

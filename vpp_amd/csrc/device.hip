@@ -169,7 +169,6 @@ DeviceBuffers* dev_upload(const HostTableSet& h, std::string* err) {
     size_t o_ip = place(h.iphash.size() * 4);
     size_t o_nimg = place(h.node_img.size() * 4);
     size_t o_nx = place(h.node_cross.size() * 4);
-    size_t o_nep = place(h.node_img_ep.size() * 4);
     std::vector<uint8_t> img(off, 0);
     auto put = [&](size_t o, const void* p, size_t n) {
         if (n) std::memcpy(img.data() + o, p, n);
@@ -181,7 +180,6 @@ DeviceBuffers* dev_upload(const HostTableSet& h, std::string* err) {
     put(o_ip, h.iphash.data(), h.iphash.size() * 4);
     put(o_nimg, h.node_img.data(), h.node_img.size() * 4);
     put(o_nx, h.node_cross.data(), h.node_cross.size() * 4);
-    put(o_nep, h.node_img_ep.data(), h.node_img_ep.size() * 4);
     auto* b = new DeviceBuffers();
     b->blob = dev_alloc(off, err);
     if (!b->blob) {
@@ -214,7 +212,6 @@ DeviceBuffers* dev_upload(const HostTableSet& h, std::string* err) {
     v.node = h.node;
     v.node.img = h.node_img.empty() ? nullptr : (const uint32_t*)(base + o_nimg);
     v.node.cross = h.node_img.empty() ? nullptr : (const uint32_t*)(base + o_nx);
-    v.node.img_ep = h.node_img_ep.empty() ? nullptr : (const uint32_t*)(base + o_nep);
     b->host_tabs = h.tabs;
     b->host_blob_words = h.blob_words;
     b->host_blob_prefix = h.blob_prefix;
@@ -448,9 +445,6 @@ constexpr size_t kLdsPerCU = 160u << 10;
 #ifndef PG_NODE_NOPAIR  // node sets without PAIR tables: the build without PAIR code (STAGE + 32)
 #define PG_NODE_NOPAIR 1
 #endif
-#ifndef PG_NODE_EPWIN  // PERPOD over such sets: dst's end point from the end-point window (STAGE + 64)
-#define PG_NODE_EPWIN 1
-#endif
 #ifndef PG_NODE_FULLH  // node kernels whose LDS histogram holds every slot: the specialised build (STAGE + 16)
 #define PG_NODE_FULLH 1
 #endif
@@ -546,9 +540,6 @@ void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
     // STAGE_ + 32 (node kernels): the node set has no PAIR tables -- the evaluation carries no
     // PAIR code (A/B on MI355X: config 5 with counters 118.9 -> 124.7 Gpps, config 3 +1 %)
     constexpr bool NOPAIR = NODE && (STAGE_ & 32);
-    // STAGE_ + 64 (PERPOD, no PAIR tables, the image staged with its end-point window): dst's
-    // end point from the window instead of its trie walk (DevNode ep_*)
-    constexpr bool EPWIN = NODE && MODE == 1 && NOPAIR && (STAGE_ & 64);
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     uint32_t* hist = smem + (STAGE ? stage_words : 0u);
     // node kernels: the LDS histogram, when used, holds every slot (HistT<true>: no window test)
@@ -721,9 +712,9 @@ void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
                 classify_candi_q<COUNT, QC>(T, LdsLoader{}, DevLoader{T.blobs + tab0.blob_off}, tab0, cs, cdp, cpr, h, co);
             } else if constexpr (NODE) {
                 if (c == (PG_HOOK_LAST ? P - QC : 0))
-                    classify_node_q<MODE, COUNT, QC, STAGE && PG_PRED, STAGE == 3, NOPAIR, EPWIN>(T, T.node, img, cs, cd, csp, cdp, cpr, h, co, hook);
+                    classify_node_q<MODE, COUNT, QC, STAGE && PG_PRED, STAGE == 3, NOPAIR>(T, T.node, img, cs, cd, csp, cdp, cpr, h, co, hook);
                 else
-                    classify_node_q<MODE, COUNT, QC, STAGE && PG_PRED, STAGE == 3, NOPAIR, EPWIN>(T, T.node, img, cs, cd, csp, cdp, cpr, h, co);
+                    classify_node_q<MODE, COUNT, QC, STAGE && PG_PRED, STAGE == 3, NOPAIR>(T, T.node, img, cs, cd, csp, cdp, cpr, h, co);
             } else {
                 classify_q<MODE, COUNT, QC, STAGE == 1 && PG_PRED>(T, blobs, tab0, cs, cd, csp, cdp, cpr, h, co, rootb);
             }
@@ -748,7 +739,7 @@ void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
         else if constexpr (FD) classify_fd_q<COUNT, 1>(T, LdsLoader{}, DevLoader{fd_blob}, tab0, s1, dp1, pr1, h, o);
         else if constexpr (MODE == 0 && STAGE == 6)
             classify_candi_q<COUNT, 1>(T, LdsLoader{}, DevLoader{T.blobs + tab0.blob_off}, tab0, s1, dp1, pr1, h, o);
-        else if constexpr (NODE) classify_node_q<MODE, COUNT, 1, STAGE && PG_PRED, STAGE == 3, NOPAIR, EPWIN>(T, T.node, img, s1, d1, sp1, dp1, pr1, h, o);
+        else if constexpr (NODE) classify_node_q<MODE, COUNT, 1, STAGE && PG_PRED, STAGE == 3, NOPAIR>(T, T.node, img, s1, d1, sp1, dp1, pr1, h, o);
         else classify_q<MODE, COUNT, 1, STAGE == 1 && PG_PRED>(T, blobs, tab0, s1, d1, sp1, dp1, pr1, h, o, rootb);
         out[i] = o[0];
     }
@@ -1105,23 +1096,7 @@ static void launch_classify(const DevTableSet& T, const Tuning& tu, int t, const
             if (nopair) return go1(std::integral_constant<int, S + 32>{}, Ts, words);
             go1(stage, Ts, words);
         };
-        // PERPOD without PAIR tables: the image copy with the end-point window (img_ep; + 64,
-        // k_classify EPWIN), staged like the image itself when the window sits over ipinfo
-        // (records left out when only that fits), else only when all of it fits
-        const bool epw = MODE == 1 && nopair && T.node.img_ep && PG_NODE_EPWIN;
-        const bool ep_in = T.node.ep_img_words == all;  // the window over ipinfo
-        DevTableSet Te = T;
-        Te.node.img = T.node.img_ep;
-        auto go_ep = [&](auto stage, uint32_t words) {
-            constexpr int S = decltype(stage)::value;
-            if (words < T.node.ep_img_words) Te.node.lrec = 0;  // (in place: the records left out)
-            if constexpr (MODE == 1) go1(std::integral_constant<int, S + 96>{}, Te, words);
-        };
-        if (epw && T.node.cmap && (fits(T.node.ep_img_words) || (ep_in && fits(norec)))) {
-            go_ep(std::integral_constant<int, 3>{}, fits(T.node.ep_img_words) ? T.node.ep_img_words : norec);
-        } else if (epw && !T.node.cmap && T.node.ep_img_words <= tu.node_stage_max_words) {
-            go_ep(std::integral_constant<int, 1>{}, T.node.ep_img_words);
-        } else if (T.node.cmap && (fits(all) || fits(norec))) {
+        if (T.node.cmap && (fits(all) || fits(norec))) {
             const uint32_t w = fits(all) ? all : norec;
             if (w < all) Tn.node.lrec = 0;
             go(std::integral_constant<int, 3>{}, Tn, w);

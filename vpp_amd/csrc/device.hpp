@@ -90,20 +90,7 @@ struct DevNode {
     // (record word p of the cross numbering is image word p - rec0 + lrec); launches that do not
     // stage that part of the image clear lrec and read the cross array
     uint32_t rec0, lrec;
-    // PERPOD end-point window (ep_span != 0): for dst in [ep_base, ep_base + ep_span), the end
-    // point of dst as one u8 (ep_wide 0) or u16 (ep_wide 1) code at byte ep_off * 4 of img_ep:
-    // the outbound table of a local pod, or kEpNode / kEpUnresolved / kEpNoAcl; any dst outside
-    // the window, and every pod of another node, is the node-output end point. PERPOD needs dst
-    // only for its end point when the node has no PAIR tables, so such launches skip dst's trie
-    // walk and its ipinfo read (one LDS byte read instead of ip_depth + 1 dependent reads).
-    // img_ep is a copy of img with the window written over ipinfo (which such launches never
-    // read), so staging it takes no more LDS than img; when the window is larger than ipinfo it
-    // is appended instead (ep_img_words > img_words: staged only when everything fits).
-    const uint32_t* img_ep;
-    uint32_t ep_base, ep_span, ep_off, ep_wide, ep_img_words;
 };
-// end-point window codes (u8 codes are these & 0xFF)
-constexpr uint32_t kEpNode = 0xFFFFu, kEpUnresolved = 0xFFFEu, kEpNoAcl = 0xFFFDu;
 
 // table sets of up to this many counter slots are counted by a full LDS histogram (one cell per
 // slot, 64 KiB with the two extra cells of a SINGLE window)
@@ -158,7 +145,6 @@ struct HostTableSet {
     int32_t node_if = -1, node_in = -1, node_out = -1;
     uint32_t slot_hot_in = 0xFFFFFFFFu;          // DevTableSet.slot_hot_in (engine.cpp compile)
     std::vector<uint32_t> node_img, node_cross;  // empty img: no node classifier
-    std::vector<uint32_t> node_img_ep;           // DevNode img_ep (empty: no end-point window)
     DevNode node{};                              // header fields (pointers unset)
     uint32_t node_rec_words = 0;                 // words of the node's dst records (build_node)
 };
@@ -182,13 +168,11 @@ struct Tuning {
     uint32_t node_root_bits = 12;  // its IPv4 / key trie root stride cap (4..16)
     uint32_t node_common = 1;      // common-row section of node images
     uint32_t fd = 1;               // FD form of dst-independent CROSS tables that fit LDS
-    uint32_t fd_l2_words = 0;      // FD blobs read from HBM: prefer a trie shape within this many words (0 = fewest levels)
     uint32_t candi = 1;            // CANDI form (inline candidates) of dst-independent HBM-resident CAND tables
     uint32_t cross_max_rules = 1u << 20;  // CROSS (cross product) considered up to this many rules (within budget)
     uint32_t node_hist_cells = 256;   // LDS slot-cache cells (rounded down to a power of two; < 16 = none)
                                       // of node launches whose set has more slots than the LDS histogram
     uint32_t node_list_words = 4096;  // node dst records up to this many words go into the image (0 = never)
-    uint32_t node_ep_window = 16384;  // PERPOD end-point window up to this many addresses (0 = none; DevNode)
     // launches
     uint32_t blocks_per_cu = 0;    // cap on resident workgroups per CU (0 = occupancy)
     uint32_t stage_max_words = kStageBlobWords;  // table blobs staged whole in LDS

@@ -52,12 +52,10 @@ const Knob kKnobs[] = {
     {"node_root_bits", &Tuning::node_root_bits, 4, 16, true},
     {"node_common", &Tuning::node_common, 0, 1, true},
     {"fd", &Tuning::fd, 0, 1, true},
-    {"fd_l2_words", &Tuning::fd_l2_words, 0, 1 << 22, true},
     {"candi", &Tuning::candi, 0, 1, true},
     {"cross_max_rules", &Tuning::cross_max_rules, 0, 1 << 24, true},
     {"node_hist_cells", &Tuning::node_hist_cells, 0, 8192, false},
     {"node_list_words", &Tuning::node_list_words, 0, 16384, true},
-    {"node_ep_window", &Tuning::node_ep_window, 0, 1 << 16, true},
     {"blocks_per_cu", &Tuning::blocks_per_cu, 0, 64, false},
     {"stage_max_words", &Tuning::stage_max_words, 0, 36864, false},
     {"node_stage_max_words", &Tuning::node_stage_max_words, 0, 36864, false},

@@ -37,7 +37,6 @@
 //   fall-through verdict, a candidate list (CAND, CANDI) flags its last record instead (no
 //   match there: the table's default deny; an empty list is one match-all record carrying it).
 #include <algorithm>
-#include <cstring>
 #include <map>
 #include <set>
 #include <unordered_map>
@@ -819,17 +818,18 @@ bool build_fd_blob(const TableAnalysis& A, uint32_t dflt, const Tuning& tu, std:
         blob[3] = s1;
         blob[4] = P;
         blob[5] = k1;
-        blob[6] = ds | dk << 8;  // reads per walk (fd_walk)
+        // reads per walk (fd_walk): each its own trie's depth when that saves 3+ reads (A/B on
+        // MI355X: the 10k-rule sweep table, src 7 / key 4 levels, 448 -> 487 Gpps; config 2's
+        // table, 4 / 2, 521 -> 510: its loop control costs more than two LDS re-reads of a self
+        // word), else both the deeper one's
+        const uint32_t dmax = std::max(ds, dk);
+        blob[6] = (dmax - std::min(ds, dk) >= 3) ? (ds | dk << 8) : (dmax | dmax << 8);
         blob[7] = 1u - kself;
         blob[8] = A.nkc;
         blob[9] = (P + K + 3u) & ~3u;
         blob[10] = A.nsc;
         if (blob.size() <= lds_words) return true;
-        // read from HBM: the fewest levels, unless Tuning::fd_l2_words asks for a blob an XCD's
-        // L2 holds -- then the first shape within it, or else the smallest
-        const bool l2 = tu.fd_l2_words != 0;
-        if (best.empty() || (l2 && best.size() > tu.fd_l2_words && blob.size() < best.size())) best.swap(blob);
-        if (l2 && best.size() <= tu.fd_l2_words) break;
+        if (best.empty()) best.swap(blob);
     }
     if (best.empty()) return false;
     blob.swap(best);
@@ -895,53 +895,11 @@ void build_common_rows(HostTableSet& h, const std::vector<uint32_t>& cov, const 
     N.img_words = (uint32_t)img.size();
 }
 
-// PERPOD end-point window (DevNode ep_*): one code per address from the lowest to the highest
-// local pod address, in a copy of the image (img_ep) over its ipinfo section when it fits there
-// (PERPOD launches that use the window never read ipinfo), else appended to that copy. Pods of
-// another node and every address outside the window take the node-output end point, like the
-// trie's node class.
-static void build_ep_window(HostTableSet& h, const std::vector<NodePod>& ps, uint32_t T, const Tuning& tu) {
-    DevNode& N = h.node;
-    N.ep_base = N.ep_span = N.ep_off = N.ep_wide = N.ep_img_words = 0;
-    h.node_img_ep.clear();
-    auto local = [](const NodePod& p) { return p.ifc < 0 || ((uint32_t)p.ifc >> kEndKindShift) == 0; };
-    uint32_t lo = 0xFFFFFFFFu, hi = 0;
-    size_t n = 0;
-    for (const NodePod& p : ps)
-        if (local(p)) lo = std::min(lo, p.ip), hi = std::max(hi, p.ip), n++;
-    if (!n || tu.node_ep_window == 0 || (uint64_t)hi - lo + 1 > tu.node_ep_window || T >= kEpNoAcl) return;
-    const bool wide = T >= (kEpNoAcl & 0xFFu);
-    const uint32_t span = hi - lo + 1;
-    std::vector<uint8_t> bytes((size_t)span * (wide ? 2 : 1), 0xFF);  // kEpNode everywhere
-    for (const NodePod& p : ps) {
-        if (!local(p)) continue;
-        const uint32_t code = p.ifc < 0 ? kEpUnresolved : (p.tout < 0 ? kEpNoAcl : (uint32_t)p.tout);
-        const size_t o = p.ip - lo;
-        if (wide) bytes[2 * o] = code & 0xFFu, bytes[2 * o + 1] = code >> 8;
-        else bytes[o] = code & 0xFFu;
-    }
-    std::vector<uint32_t>& img = h.node_img_ep;
-    img = h.node_img;
-    if (bytes.size() <= (size_t)N.n_ipc * 8u) {  // over ipinfo (uint2 per IP class)
-        N.ep_off = N.ipinfo;
-    } else {
-        while (img.size() % 4) img.push_back(0);
-        N.ep_off = (uint32_t)img.size();
-        img.resize(img.size() + (bytes.size() + 15) / 16 * 4, 0);
-    }
-    std::memcpy(img.data() + N.ep_off, bytes.data(), bytes.size());
-    N.ep_img_words = (uint32_t)img.size();
-    N.ep_base = lo;
-    N.ep_span = span;
-    N.ep_wide = wide;
-}
-
 bool build_node(HostTableSet& h, const std::vector<TableAnalysis*>& an, const std::vector<NodePod>& pods,
                 const NodePod& node_end, const Tuning& tu) {
     h.node_img.clear();
     h.node_cross.clear();
     h.node = DevNode{};
-    h.node_img_ep.clear();
     h.node_rec_words = 0;
     const uint32_t T = (uint32_t)h.tabs.size();
     if (!tu.node_build || T == 0 || T >= 0xFFFFu) return false;
@@ -1168,7 +1126,6 @@ bool build_node(HostTableSet& h, const std::vector<TableAnalysis*>& an, const st
         img.insert(img.end(), recs.begin(), recs.end());
         N.img_words = (uint32_t)img.size();
     }
-    build_ep_window(h, ps, T, tu);
     if (X.empty()) X.resize(4, 0);
     return true;
 }

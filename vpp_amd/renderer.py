@@ -287,10 +287,9 @@ class Engine:
         return out
 
     def debug_classify_host(self, mode, table_id, src, dst, sport, dport, proto, counters=False, node=True,
-                            pred=True, common=True, epwin=False):
+                            pred=True, common=True):
         """TESTS ONLY: pg_classify's per-tuple code run on the host (pg_debug_classify_host).
-        ``common``: the node image's common-row section (when it was built); ``epwin``: PERPOD
-        dst end points from the node's end-point window (when built; no PAIR tables).
+        ``common``: the node image's common-row section (when it was built).
         -> verdict words (u32), and the u64 hit counters when ``counters``."""
         import numpy as np
         n = len(src)
@@ -302,8 +301,7 @@ class Engine:
         cnt = np.zeros(self.num_counter_slots(), np.uint64) if counters else None
         self._ck(lib.pg_debug_classify_host(self.h, mode, table_id, C.byref(t), n, p(out),
                                             p(cnt) if counters else None,
-                                            int(node) | (2 if pred else 0) | (4 if common else 0) |
-                                            (8 if epwin else 0)))
+                                            int(node) | (2 if pred else 0) | (4 if common else 0)))
         return (out, cnt) if counters else out
 
     def debug_walk_stats(self, table_id, src, dst, dport, proto):
@@ -335,9 +333,6 @@ class Engine:
         rb, inimg = C.c_uint64(), C.c_int()
         self._ck(lib.pg_node_list_stats(self.h, C.byref(rb), C.byref(inimg)))
         st.update(list_record_bytes=rb.value, list_records_in_image=bool(inimg.value))
-        eb, es, ew = C.c_uint32(), C.c_uint32(), C.c_int()
-        self._ck(lib.pg_node_ep_stats(self.h, C.byref(eb), C.byref(es), C.byref(ew)))
-        st.update(ep_window_base=eb.value, ep_window_addresses=es.value, ep_window_wide=bool(ew.value))
         return st
 
     def slot_of_rule(self, tid, idx):
