@@ -31,6 +31,9 @@ namespace pg {
 #ifndef PG_FD_SKIP  // FD walks over a blob in HBM: no re-read of a finished lane's self word
 #define PG_FD_SKIP 1
 #endif
+#ifndef PG_MUL24  // node cross-entry index products as 24-bit multiplies
+#define PG_MUL24 1
+#endif
 #ifndef PG_NODE_FB_Q1  // node kernels: per-table fallback one tuple at a time
 #define PG_NODE_FB_Q1 1
 #endif
@@ -44,6 +47,15 @@ PG_HD uint32_t pkt_key(uint32_t proto, uint32_t port) {
     return (p << 16) | (p < 2u ? port : 0u);
 }
 PG_HD uint32_t verdict(uint32_t act, uint32_t slot) { return (act << 30) | slot; }
+// a * b for operands below 2^16 (class indices x row widths): one full-rate 24-bit multiply on
+// the device, where the compiler otherwise emits a 64-bit multiply-add for the u32 product
+PG_HD uint32_t mul24(uint32_t a, uint32_t b) {
+#if defined(__HIP_DEVICE_COMPILE__) && PG_MUL24
+    return __umul24(a, b);
+#else
+    return a * b;
+#endif
+}
 constexpr uint32_t kSlotMask = 0x3FFFFFFFu;
 
 PG_HD uint32_t hash_ip(uint32_t ip) {
@@ -639,7 +651,7 @@ struct NodeEval {
             if (CM) cw = img.u32(N.cmap + (tt << N.cmap_shift) + (ca[j] >> 5u)) >> (ca[j] & 31u);
             on[j] = act[j] && k[j] < kWalkKeyLimit && (ti.y >> 31);
             cm[j] = CM && (cw & 1u);
-            pos[j] = cm[j] ? ti.z + lk : ti.x + ca[j] * (ti.y & 0xFFFFu) + lk;
+            pos[j] = cm[j] ? ti.z + lk : ti.x + mul24(ca[j], ti.y & 0xFFFFu) + lk;
             fb[j] = act[j] && !on[j];
             // PAIR table (kNodePairFlag): the pair map entry first, its verdict row after (a
             // uniform test first: node sets without PAIR tables skip this code)
@@ -647,7 +659,7 @@ struct NodeEval {
             if (pr[j]) {
                 const uint32_t mo = ti.w & 0xFFFFu;
                 const uint32_t sc = img.u32(mo + ca[j]) & 0xFFFFu, dc = img.u32(mo + cb[j]) >> 16;
-                pos[j] = ti.x + sc * (ti.w >> 16) + dc;
+                pos[j] = ti.x + mul24(sc, ti.w >> 16) + dc;
                 pv[j] = ti.z + lk;
                 pk[j] = ti.y & 0xFFFFu;
             }
