@@ -658,35 +658,21 @@ void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
     constexpr int PF = (!NODE && PF0 == 2) ? 1 : PF0;  // (only node kernels have the gather hook)
     // PD = 2 (PG_PF_DEPTH): the loads run two groups ahead (group q + 2 * stride is
     // loaded while group q is classified). PF 3: the loads are issued after the group's
-    // classification (its gathers waited for), just before its verdict store. Vector-memory
+    // classification (its gathers waited for) and verdict store. Vector-memory
     // operations retire in issue order (MI355X_MICROARCH.md, vmcnt), so a cross-table gather
     // issued after a stream load waits for that load too.
     constexpr int PD = PF ? PG_PF_DEPTH : 1;
-    Group ahead{};
-    if (PF && q < nfull) cur = load(q);
-    if (PD == 2 && q + stride < nfull) ahead = load(q + stride);
-    while (q < nfull) {
-        const uint64_t qn = q + stride, qa = PD == 2 ? qn + stride : qn;  // qa: the group loaded now
-        Group nxt = PD == 2 ? ahead : cur;
-        if (!PF) cur = load(q);
-        auto issue = [&]() {
-            if (qa < nfull) {
-                if constexpr (PD == 2) ahead = load(qa);
-                else nxt = load(qa);
-            }
-        };
-        if (PF == 1) issue();
-        [[maybe_unused]] auto hook = [&]() {
-            if (PF == 2) issue();
-        };
+    // classification of one group (P tuples per lane, loaded), its verdicts stored; hk: called
+    // once after the first chunk's cross-entry loads are issued (node kernels, PF 2)
+    auto run_group = [&](const Group& g, uint64_t qq, auto&& hk) {
         uint32_t sv[P], dv[P], spv[P], dpv[P], prv[P], o[P];
 #pragma unroll
         for (int j = 0; j < P; j++) {
-            sv[j] = cur.s.w[j];
-            dv[j] = cur.d.w[j];
-            dpv[j] = (cur.dp.w[j / 2] >> (16 * (j & 1))) & 0xFFFFu;
-            spv[j] = (cur.sp.w[j / 2] >> (16 * (j & 1))) & 0xFFFFu;
-            prv[j] = (cur.pr.w[j / 4] >> (8 * (j & 3))) & 0xFFu;
+            sv[j] = g.s.w[j];
+            dv[j] = g.d.w[j];
+            dpv[j] = (g.dp.w[j / 2] >> (16 * (j & 1))) & 0xFFFFu;
+            spv[j] = (g.sp.w[j / 2] >> (16 * (j & 1))) & 0xFFFFu;
+            prv[j] = (g.pr.w[j / 4] >> (8 * (j & 3))) & 0xFFu;
         }
 #if PG_PROBE_STREAM
         for (int j = 0; j < P; j++) o[j] = sv[j] ^ dv[j] ^ dpv[j] ^ prv[j] ^ spv[j];
@@ -712,7 +698,7 @@ void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
                 classify_candi_q<COUNT, QC>(T, LdsLoader{}, DevLoader{T.blobs + tab0.blob_off}, tab0, cs, cdp, cpr, h, co);
             } else if constexpr (NODE) {
                 if (c == (PG_HOOK_LAST ? P - QC : 0))
-                    classify_node_q<MODE, COUNT, QC, STAGE && PG_PRED, STAGE == 3, NOPAIR>(T, T.node, img, cs, cd, csp, cdp, cpr, h, co, hook);
+                    classify_node_q<MODE, COUNT, QC, STAGE && PG_PRED, STAGE == 3, NOPAIR>(T, T.node, img, cs, cd, csp, cdp, cpr, h, co, hk);
                 else
                     classify_node_q<MODE, COUNT, QC, STAGE && PG_PRED, STAGE == 3, NOPAIR>(T, T.node, img, cs, cd, csp, cdp, cpr, h, co);
             } else {
@@ -722,11 +708,30 @@ void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
             for (int j = 0; j < QC; j++) o[c + j] = co[j];
         }
 #endif
-        if (PF == 3) issue();
         Words<P> ow;
 #pragma unroll
         for (int j = 0; j < P; j++) ow.w[j] = o[j];
-        st_words<P>(ow, out + q * P);
+        st_words<P>(ow, out + qq * P);
+    };
+    Group ahead{};
+    if (PF && q < nfull) cur = load(q);
+    if (PD == 2 && q + stride < nfull) ahead = load(q + stride);
+    while (q < nfull) {
+        const uint64_t qn = q + stride, qa = PD == 2 ? qn + stride : qn;  // qa: the group loaded now
+        Group nxt = PD == 2 ? ahead : cur;
+        if (!PF) cur = load(q);
+        auto issue = [&]() {
+            if (qa < nfull) {
+                if constexpr (PD == 2) ahead = load(qa);
+                else nxt = load(qa);
+            }
+        };
+        if (PF == 1) issue();
+        auto hook = [&]() {
+            if (PF == 2) issue();
+        };
+        run_group(cur, q, hook);
+        if (PF == 3) issue();  // (the loads after the group's classification and verdict store)
         cur = nxt;
         q = qn;
     }
