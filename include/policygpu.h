@@ -167,7 +167,8 @@ int pg_ctx_device(const pg_ctx* ctx);
  * 12), "candi" (1/0: candidates inline in the 8-B trie entries of HBM-resident candidate tables
  * no live rule of which tests dst, default 1), "fd" (1/0: fixed-depth form of dst-independent
  * cross-product tables, default 1), "node_common" (1/0: common-row section of node
- * images, default 1), "node_list_words" (node dst records -- the dst-specific rules a node
+ * images, default 1), "node_uniform" (1/0: the node's uniform cross layout where every table
+ * is covered and none is in PAIR form, default 1), "node_list_words" (node dst records -- the dst-specific rules a node
  * cross entry must still test -- up to this many words go into the node image, so a launch that
  * stages the image walks them in LDS; default 4096, 0 = never), "pair" (1/0: the PAIR structure -- src x dst classes, then x key classes
  * -- for tables the cross product cannot take, default 1; 0 = candidate lists; 2 = wherever it
@@ -269,6 +270,10 @@ int pg_node_common_stats(pg_ctx* ctx, uint64_t* base_image_bytes, uint64_t* comm
 /* the node classifier's dst records (the dst-specific rules its cross entries still test): their
  * bytes, and whether a copy ends the node image (tuning "node_list_words"); PG_ENOENT: no node */
 int pg_node_list_stats(pg_ctx* ctx, uint64_t* record_bytes, int* in_image);
+/* 1 when the node classifier uses the uniform cross layout (every table covered, none in PAIR
+ * form, tuning "node_uniform": entry addresses computed, no per-table info reads), else 0;
+ * PG_ENOENT: no node */
+int pg_node_uniform(pg_ctx* ctx);
 /* reference-shaped linear-scan kernel (K1) on one table, for validation and comparison */
 int pg_classify_linear(pg_ctx* ctx, int table_id, const pg_tuple_soa* tuples, uint64_t n, uint32_t* out,
                        void* hip_stream);

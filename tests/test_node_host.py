@@ -181,6 +181,8 @@ def test_config3_cluster_node_path():
     assert np.array_equal(got0, got)
     # the global table's dst-specific rules: dst records, a copy at the end of the image
     assert ns["list_record_bytes"] > 0 and ns["list_records_in_image"], ns
+    # every table covered, none in PAIR form: the uniform cross layout
+    assert ns["uniform"], ns
 
 
 def test_node_dst_records_in_image_or_cross():
@@ -263,3 +265,24 @@ def test_config6_pair_table_covered():
     act, slot = wd.perpod(src, dst, dport, proto, threads=8)
     got = e.debug_classify_host(MODE_PERPOD, -1, src, dst, sport, dport, proto, node=True)
     assert np.array_equal(got >> 30, act.astype(np.uint32)) and np.array_equal(got & 0x3FFFFFFF, slot)
+
+
+@pytest.mark.parametrize("config", [3, 5])
+def test_uniform_cross_layout_equals_per_table_layout(config):
+    """The node's uniform cross layout (rows over the node key classes, addresses computed) and
+    the per-table layout (node_uniform=0: tabinfo / kmap reads) classify the same, counters
+    included, with and without the common-row section."""
+    w = W.CONFIGS[config](0, n_tuples=1 << 10, n_ns=4)
+    e = w.engine
+    assert e.node_stats()["uniform"]
+    src, dst, sport, dport, proto = gen.gen_tuples(40003, **w.gen)
+    ref = {cm: e.debug_classify_host(w.mode, -1, src, dst, sport, dport, proto, counters=True, node=True, common=cm)
+           for cm in (True, False)}
+    with e.tuning(node_uniform=0):
+        assert not e.node_stats()["uniform"]
+        for cm in (True, False):
+            got, cnt = e.debug_classify_host(w.mode, -1, src, dst, sport, dport, proto, counters=True, node=True,
+                                             common=cm)
+            assert np.array_equal(got, ref[cm][0]) and np.array_equal(cnt, ref[cm][1])
+    per_table = e.debug_classify_host(w.mode, -1, src, dst, sport, dport, proto, node=False)
+    assert np.array_equal(per_table, ref[True][0])

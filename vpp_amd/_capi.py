@@ -167,6 +167,7 @@ _SIGS = {
                                 C.POINTER(C.c_uint64)]),
     "pg_node_common_stats": (C.c_int, [_P, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
     "pg_node_list_stats": (C.c_int, [_P, C.POINTER(C.c_uint64), C.POINTER(C.c_int)]),
+    "pg_node_uniform": (C.c_int, [_P]),
     "pg_configurator_new": (_P, []),
     "pg_configurator_free": (None, [_P]),
     "pg_configurator_last_error": (C.c_char_p, [_P]),

@@ -636,7 +636,7 @@ DevTableSet host_view(const HostTableSet& h) {
     return v;
 }
 
-template <int MODE, int Q, bool PRED, bool CM>
+template <int MODE, int Q, bool PRED, bool CM, bool UNI>
 void host_q(const DevTableSet& T, bool node, int table_id, const pg_tuple_soa* t, uint64_t i, uint32_t* out,
             const Hist& h) {
     uint32_t s[Q], d[Q], sp[Q], dp[Q], pr[Q], o[Q];
@@ -653,26 +653,26 @@ void host_q(const DevTableSet& T, bool node, int table_id, const pg_tuple_soa* t
             classify_q<0, true, Q, PRED>(T, T.blobs, tab, s, d, sp, dp, pr, h, o);
         }
     } else {
-        if (node) classify_node_q<MODE, true, Q, PRED, CM>(T, T.node, DevLoader{T.node.img}, s, d, sp, dp, pr, h, o);
+        if (node) classify_node_q<MODE, true, Q, PRED, CM, false, UNI>(T, T.node, DevLoader{T.node.img}, s, d, sp, dp, pr, h, o);
         else classify_q<MODE, true, Q, PRED>(T, T.blobs, DevTable{}, s, d, sp, dp, pr, h, o);
     }
     for (int j = 0; j < Q; j++) out[i + j] = o[j];
 }
 
-template <int MODE, bool PRED, bool CM>
+template <int MODE, bool PRED, bool CM, bool UNI>
 void host_classify(const DevTableSet& T, bool node, int table_id, const pg_tuple_soa* t, uint64_t n, uint32_t* out,
                    const Hist& h) {
     const uint64_t nq = n & ~(uint64_t)3;  // the kernels' quads, then one tuple at a time
-    for (uint64_t i = 0; i < nq; i += 4) host_q<MODE, 4, PRED, CM>(T, node, table_id, t, i, out, h);
-    for (uint64_t i = nq; i < n; i++) host_q<MODE, 1, PRED, CM>(T, node, table_id, t, i, out, h);
+    for (uint64_t i = 0; i < nq; i += 4) host_q<MODE, 4, PRED, CM, UNI>(T, node, table_id, t, i, out, h);
+    for (uint64_t i = nq; i < n; i++) host_q<MODE, 1, PRED, CM, UNI>(T, node, table_id, t, i, out, h);
 }
-template <int MODE>
+template <int MODE, bool UNI>
 void host_classify(const DevTableSet& T, bool node, bool pred, bool cm, int table_id, const pg_tuple_soa* t,
                    uint64_t n, uint32_t* out, const Hist& h) {
-    if (pred && cm) host_classify<MODE, true, true>(T, node, table_id, t, n, out, h);
-    else if (pred) host_classify<MODE, true, false>(T, node, table_id, t, n, out, h);
-    else if (cm) host_classify<MODE, false, true>(T, node, table_id, t, n, out, h);
-    else host_classify<MODE, false, false>(T, node, table_id, t, n, out, h);
+    if (pred && cm) host_classify<MODE, true, true, UNI>(T, node, table_id, t, n, out, h);
+    else if (pred) host_classify<MODE, true, false, UNI>(T, node, table_id, t, n, out, h);
+    else if (cm) host_classify<MODE, false, true, UNI>(T, node, table_id, t, n, out, h);
+    else host_classify<MODE, false, false, UNI>(T, node, table_id, t, n, out, h);
 }
 }  // namespace
 
@@ -693,9 +693,12 @@ int pg_debug_classify_host(pg_ctx* ctx, int mode, int table_id, const pg_tuple_s
     const bool use_node = (node & 1) && T.node.img != nullptr, pred = (node & 2) != 0;
     const bool cm = use_node && (node & 4) && T.node.cmap != 0;
     const Hist h{nullptr, (unsigned long long*)counters};
-    if (mode == 0) host_classify<0>(T, false, pred, false, table_id, t, n, out, h);
-    else if (mode == 1) host_classify<1>(T, use_node, pred, cm, table_id, t, n, out, h);
-    else host_classify<2>(T, use_node, pred, cm, table_id, t, n, out, h);
+    const bool uni = use_node && T.node.uniform;  // the layout the node was built with
+    if (mode == 0) host_classify<0, false>(T, false, pred, false, table_id, t, n, out, h);
+    else if (mode == 1 && uni) host_classify<1, true>(T, use_node, pred, cm, table_id, t, n, out, h);
+    else if (mode == 1) host_classify<1, false>(T, use_node, pred, cm, table_id, t, n, out, h);
+    else if (uni) host_classify<2, true>(T, use_node, pred, cm, table_id, t, n, out, h);
+    else host_classify<2, false>(T, use_node, pred, cm, table_id, t, n, out, h);
     return PG_OK;
     GUARD_END(ctx)
 }
@@ -759,6 +762,16 @@ int pg_node_list_stats(pg_ctx* ctx, uint64_t* record_bytes, int* in_image) {
     if (record_bytes) *record_bytes = (uint64_t)h.node_rec_words * 4;
     if (in_image) *in_image = h.node.lrec != 0;
     return PG_OK;
+    GUARD_END(ctx)
+}
+
+int pg_node_uniform(pg_ctx* ctx) {
+    if (!ctx) return PG_EINVAL;
+    GUARD_BEGIN
+    Engine& E = ctx->eng;
+    if (!E.compiled) E.compile();
+    if (E.host.node_img.empty()) return fail(ctx, PG_ENOENT, "no node classifier (disabled or over budget)");
+    return E.host.node.uniform ? 1 : 0;
     GUARD_END(ctx)
 }
 

@@ -608,7 +608,8 @@ struct NoHook {
 // CM: the node image's common-row section is in use (device.hpp DevNode): evaluations whose
 // (table, IP class) row is the table's common row read it from the image, not the cross table.
 // NP: the node set has no PAIR tables (the launcher's build for it: no PAIR code at all)
-template <class L, int Q, class H = NoHook, bool CM = false, bool NP = false>
+// UNI: the node's uniform cross layout (DevNode uniform; implies NP): entry addresses computed
+template <class L, int Q, class H = NoHook, bool CM = false, bool NP = false, bool UNI = false>
 struct NodeEval {
     const DevTableSet& T;
     const DevNode& N;
@@ -641,6 +642,19 @@ struct NodeEval {
         const uint32_t(&gk)[Q] = rev ? gack : gsyn;
         bool cm[Q], pr[Q];
         uint32_t pos[Q], pv[Q] = {}, pk[Q] = {};
+        if constexpr (UNI) {  // every table covered, none in PAIR form: no tabinfo / kmap reads
+            PG_UNROLL
+            for (int j = 0; j < Q; j++) {
+                const uint32_t tt = act[j] ? (uint32_t)t[j] : 0u;
+                uint32_t cw = 0;
+                if (CM) cw = img.u32(N.cmap + (tt << N.cmap_shift) + (ca[j] >> 5u)) >> (ca[j] & 31u);
+                on[j] = act[j] && k[j] < kWalkKeyLimit;
+                cm[j] = CM && (cw & 1u);
+                pos[j] = cm[j] ? N.crow0 + mul24(tt, N.gk) + gk[j] : mul24(mul24(tt, N.n_ipc) + ca[j], N.gk) + gk[j];
+                fb[j] = act[j] && !on[j];
+                pr[j] = false;
+            }
+        } else {
         // branch-free: every lane reads its (or table 0's) image words, the flags select
         PG_UNROLL
         for (int j = 0; j < Q; j++) {
@@ -663,6 +677,7 @@ struct NodeEval {
                 pv[j] = ti.z + lk;
                 pk[j] = ti.y & 0xFFFFu;
             }
+        }
         }
         PG_UNROLL
         for (int j = 0; j < Q; j++) {
@@ -927,8 +942,8 @@ PG_HD void classify_q(const DevTableSet& T, const uint32_t* blobs, const DevTabl
 
 // Q tuples of one lane, PERPOD / CONN, node path. `img` reads the node image (LDS copy or
 // global memory).
-template <int MODE, bool COUNT, int Q, bool PRED = false, bool CM = false, bool NP = false, class L, class HS,
-          class H = NoHook>
+template <int MODE, bool COUNT, int Q, bool PRED = false, bool CM = false, bool NP = false, bool UNI = false,
+          class L, class HS, class H = NoHook>
 PG_HD void classify_node_q(const DevTableSet& T, const DevNode& N, const L& img, const uint32_t (&s)[Q],
                            const uint32_t (&d)[Q], const uint32_t (&sp)[Q], const uint32_t (&dp)[Q],
                            const uint32_t (&pr)[Q], const HS& h, uint32_t (&out)[Q], const H& hook = H()) {
@@ -999,7 +1014,7 @@ PG_HD void classify_node_q(const DevTableSet& T, const DevNode& N, const L& img,
     PG_UNROLL
     for (int j = 0; j < Q; j++) cs[j] = ipc[j], cd[j] = ipc[Q + j];
     bool hooked = false;
-    const NodeEval<L, Q, H, CM, NP> ev{T, N, img, s, d, key, kack, cs, cd, gs, ga, hook, &hooked};
+    const NodeEval<L, Q, H, CM, NP || UNI, UNI> ev{T, N, img, s, d, key, kack, cs, cd, gs, ga, hook, &hooked};
     if (MODE == 1) {
         int32_t t[Q];
         bool run[Q];

@@ -540,6 +540,8 @@ void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
     // STAGE_ + 32 (node kernels): the node set has no PAIR tables -- the evaluation carries no
     // PAIR code (A/B on MI355X: config 5 with counters 118.9 -> 124.7 Gpps, config 3 +1 %)
     constexpr bool NOPAIR = NODE && (STAGE_ & 32);
+    // STAGE_ + 64 (node kernels): the node's uniform cross layout (DevNode uniform; with + 32)
+    constexpr bool UNIF = NODE && NOPAIR && (STAGE_ & 64);
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     uint32_t* hist = smem + (STAGE ? stage_words : 0u);
     // node kernels: the LDS histogram, when used, holds every slot (HistT<true>: no window test)
@@ -698,9 +700,9 @@ void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
                 classify_candi_q<COUNT, QC>(T, LdsLoader{}, DevLoader{T.blobs + tab0.blob_off}, tab0, cs, cdp, cpr, h, co);
             } else if constexpr (NODE) {
                 if (c == (PG_HOOK_LAST ? P - QC : 0))
-                    classify_node_q<MODE, COUNT, QC, STAGE && PG_PRED, STAGE == 3, NOPAIR>(T, T.node, img, cs, cd, csp, cdp, cpr, h, co, hk);
+                    classify_node_q<MODE, COUNT, QC, STAGE && PG_PRED, STAGE == 3, NOPAIR, UNIF>(T, T.node, img, cs, cd, csp, cdp, cpr, h, co, hk);
                 else
-                    classify_node_q<MODE, COUNT, QC, STAGE && PG_PRED, STAGE == 3, NOPAIR>(T, T.node, img, cs, cd, csp, cdp, cpr, h, co);
+                    classify_node_q<MODE, COUNT, QC, STAGE && PG_PRED, STAGE == 3, NOPAIR, UNIF>(T, T.node, img, cs, cd, csp, cdp, cpr, h, co);
             } else {
                 classify_q<MODE, COUNT, QC, STAGE == 1 && PG_PRED>(T, blobs, tab0, cs, cd, csp, cdp, cpr, h, co, rootb);
             }
@@ -744,7 +746,7 @@ void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
         else if constexpr (FD) classify_fd_q<COUNT, 1>(T, LdsLoader{}, DevLoader{fd_blob}, tab0, s1, dp1, pr1, h, o);
         else if constexpr (MODE == 0 && STAGE == 6)
             classify_candi_q<COUNT, 1>(T, LdsLoader{}, DevLoader{T.blobs + tab0.blob_off}, tab0, s1, dp1, pr1, h, o);
-        else if constexpr (NODE) classify_node_q<MODE, COUNT, 1, STAGE && PG_PRED, STAGE == 3, NOPAIR>(T, T.node, img, s1, d1, sp1, dp1, pr1, h, o);
+        else if constexpr (NODE) classify_node_q<MODE, COUNT, 1, STAGE && PG_PRED, STAGE == 3, NOPAIR, UNIF>(T, T.node, img, s1, d1, sp1, dp1, pr1, h, o);
         else classify_q<MODE, COUNT, 1, STAGE == 1 && PG_PRED>(T, blobs, tab0, s1, d1, sp1, dp1, pr1, h, o, rootb);
         out[i] = o[0];
     }
@@ -1086,6 +1088,8 @@ static void launch_classify(const DevTableSet& T, const Tuning& tu, int t, const
         const bool full = PG_NODE_FULLH && COUNT && T.n_slots <= kLdsHistMax - 2u;
         // (+ 32: the set has no PAIR tables, k_classify NOPAIR)
         const bool nopair = T.node.n_pair == 0 && PG_NODE_NOPAIR;
+        // (+ 64: the uniform cross layout, k_classify UNIF)
+        const bool unif = nopair && T.node.uniform;
         auto go1 = [&](auto stage, const DevTableSet& Ts, uint32_t words) {
             constexpr int S = decltype(stage)::value;
             if constexpr (COUNT) {
@@ -1098,6 +1102,7 @@ static void launch_classify(const DevTableSet& T, const Tuning& tu, int t, const
         };
         auto go = [&](auto stage, const DevTableSet& Ts, uint32_t words) {
             constexpr int S = decltype(stage)::value;
+            if (unif) return go1(std::integral_constant<int, S + 96>{}, Ts, words);
             if (nopair) return go1(std::integral_constant<int, S + 32>{}, Ts, words);
             go1(stage, Ts, words);
         };

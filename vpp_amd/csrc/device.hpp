@@ -90,6 +90,11 @@ struct DevNode {
     // (record word p of the cross numbering is image word p - rec0 + lrec); launches that do not
     // stage that part of the image clear lrec and read the cross array
     uint32_t rec0, lrec;
+    // uniform layout (every table covered, none in PAIR form; Tuning::node_uniform): table t's
+    // cross rows are over the node key classes, entry (t, ip class g, key class k) at word
+    // (t * n_ipc + g) * gk + k, and its common row (when cmap != 0) at image word crow0 + t * gk;
+    // tabinfo and kmap are not read
+    uint32_t uniform, crow0;
 };
 
 // table sets of up to this many counter slots are counted by a full LDS histogram (one cell per
@@ -173,6 +178,7 @@ struct Tuning {
     uint32_t node_hist_cells = 256;   // LDS slot-cache cells (rounded down to a power of two; < 16 = none)
                                       // of node launches whose set has more slots than the LDS histogram
     uint32_t node_list_words = 4096;  // node dst records up to this many words go into the image (0 = never)
+    uint32_t node_uniform = 1;        // the node's uniform cross layout where it applies (DevNode uniform)
     // launches
     uint32_t blocks_per_cu = 0;    // cap on resident workgroups per CU (0 = occupancy)
     uint32_t stage_max_words = kStageBlobWords;  // table blobs staged whole in LDS

@@ -56,6 +56,7 @@ const Knob kKnobs[] = {
     {"cross_max_rules", &Tuning::cross_max_rules, 0, 1 << 24, true},
     {"node_hist_cells", &Tuning::node_hist_cells, 0, 8192, false},
     {"node_list_words", &Tuning::node_list_words, 0, 16384, true},
+    {"node_uniform", &Tuning::node_uniform, 0, 1, true},
     {"blocks_per_cu", &Tuning::blocks_per_cu, 0, 64, false},
     {"stage_max_words", &Tuning::stage_max_words, 0, 36864, false},
     {"node_stage_max_words", &Tuning::node_stage_max_words, 0, 36864, false},

@@ -852,7 +852,7 @@ bool build_fd_blob(const TableAnalysis& A, uint32_t dflt, const Tuning& tu, std:
 // budget allows (device.hip). Skipped when the bitmap would exceed kCommonMapMaxBits.
 constexpr uint64_t kCommonMapMaxBits = 1ull << 20;  // 128 KiB
 void build_common_rows(HostTableSet& h, const std::vector<uint32_t>& cov, const std::vector<TableAnalysis*>& an,
-                       const Tuning& tu) {
+                       const Tuning& tu, bool uni) {
     std::vector<uint32_t>& img = h.node_img;
     DevNode& N = h.node;
     const uint32_t T = (uint32_t)h.tabs.size(), G = N.n_ipc;
@@ -864,7 +864,7 @@ void build_common_rows(HostTableSet& h, const std::vector<uint32_t>& cov, const 
     std::vector<uint32_t> sec, map((size_t)(bits / 32), 0);
     std::vector<uint32_t> crow(T, 0);
     for (uint32_t t : cov) {
-        const uint32_t base = img[N.tabinfo + 4 * t], nk = an[t]->nkc;
+        const uint32_t base = img[N.tabinfo + 4 * t], nk = uni ? N.gk : an[t]->nkc;
         // most frequent row: rows hashed, candidates compared word by word
         std::unordered_map<uint64_t, std::pair<uint32_t, uint32_t>> freq;  // hash -> (first ip class, count)
         auto row = [&](uint32_t g) { return X.data() + base + (size_t)g * nk; };
@@ -990,6 +990,12 @@ bool build_node(HostTableSet& h, const std::vector<TableAnalysis*>& an, const st
         kcls[k] = it->second;
     }
     const uint32_t GK = (uint32_t)kc_key.size();
+    // uniform layout (DevNode uniform): every table covered, none in PAIR form -- rows over the
+    // node key classes at cross[(t * G + ip class) * GK + key class], so an evaluation computes
+    // its entry's address from (t, classes) instead of reading tabinfo and kmap
+    const bool uni = tu.node_uniform && C == T && PC == 0 && (uint64_t)T * G < (1u << 24) &&
+                     (uint64_t)T * G * GK <= kNodeCrossBudget;
+    if (uni) entries = (uint64_t)T * G * GK;
 
     // image: tries, ipinfo, tabinfo, kmap
     std::vector<uint32_t>& img = h.node_img;
@@ -1079,9 +1085,11 @@ bool build_node(HostTableSet& h, const std::vector<TableAnalysis*>& an, const st
             continue;
         }
         std::vector<uint32_t> first(A.clist.empty() ? 0 : A.cverd.size(), 0xFFFFFFFFu);
+        const uint32_t nkr = uni ? GK : A.nkc;  // row width: node key classes (uniform) or the table's
         for (uint32_t g = 0; g < G; g++) {
             const uint32_t sc = ipc_key[g][3 + c];
-            for (uint32_t lk = 0; lk < A.nkc; lk++) {
+            for (uint32_t x = 0; x < nkr; x++) {
+                const uint32_t lk = uni ? kc_key[x][c] : x;
                 const size_t e = (size_t)sc * A.nkc + lk;
                 if (A.clist.empty() || A.clist[e].empty()) {
                     X.push_back(A.cverd[e]);
@@ -1110,7 +1118,9 @@ bool build_node(HostTableSet& h, const std::vector<TableAnalysis*>& an, const st
     std::vector<uint32_t> xcov;  // the cross-product tables (common rows); PAIR tables have none
     for (uint32_t t : cov)
         if (!an[t]->pair) xcov.push_back(t);
-    build_common_rows(h, xcov, an, tu);
+    build_common_rows(h, xcov, an, tu, uni);
+    N.uniform = uni;
+    N.crow0 = uni && N.cmap ? img[N.tabinfo + 2] : 0;  // table 0's common row: table t's at crow0 + t * GK
     X.resize(rec0, 0);
     X.insert(X.end(), recs.begin(), recs.end());
     // dst records, also at the end of the image when they fit node_list_words: a launch that
