@@ -417,6 +417,9 @@ constexpr size_t kLdsPerCU = 160u << 10;
 #ifndef PG_QPOD  // PERPOD: 2 (A/B on MI355X, config 3: 237 vs 198 Gpps at 4 -- fewer registers)
 #define PG_QPOD 2
 #endif
+#ifndef PG_QPOD_FULLH  // PERPOD counting into an LDS histogram of every slot (64 registers, 1024
+#define PG_QPOD_FULLH 4     // threads): 4 (A/B on MI355X, config 3 with counters 282 -> 295 Gpps)
+#endif
 #ifndef PG_QCONN
 #define PG_QCONN 1
 #endif
@@ -682,7 +685,7 @@ void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
         // per-mode chunk: the group's P tuples are classified QC at a time (less state per
         // lane, more waves per SIMD)
         constexpr int QC = MODE == 2 ? (COUNT ? PG_QCONN_COUNT : PG_QCONN)
-                                     : (MODE == 1 ? PG_QPOD
+                                     : (MODE == 1 ? (FULLH ? PG_QPOD_FULLH : PG_QPOD)
                                                   : (FD ? (STAGE == 4 ? PG_QSINGLE_FD : PG_QSINGLE_FDG)
                                                         : (STAGE == 1   ? PG_QSINGLE_LDS
                                                            : STAGE == 6 ? (COUNT ? PG_QSINGLE : PG_QCANDI)
