@@ -624,6 +624,9 @@ struct NodeEval {
     const uint32_t (&gack)[Q];
     const H& hook;
     bool* hooked;
+    // UNI with common rows: the common-row masks of the src and dst IP classes (DevNode uniform)
+    const W2 (*msk_s)[Q] = nullptr;
+    const W2 (*msk_d)[Q] = nullptr;
     PG_HD void operator()(const int32_t (&t)[Q], const bool (&act)[Q], bool rev, uint32_t (&w)[Q]) const {
         bool on[Q], fb[Q];
         first(t, act, rev, on, fb, w);
@@ -647,7 +650,10 @@ struct NodeEval {
             for (int j = 0; j < Q; j++) {
                 const uint32_t tt = act[j] ? (uint32_t)t[j] : 0u;
                 uint32_t cw = 0;
-                if (CM) cw = img.u32(N.cmap + (tt << N.cmap_shift) + (ca[j] >> 5u)) >> (ca[j] & 31u);
+                if (CM) {  // bit t of the rule-src-side class's mask
+                    const W2 m = rev ? (*msk_d)[j] : (*msk_s)[j];
+                    cw = (tt < 32u ? m.x : m.y) >> (tt & 31u);
+                }
                 on[j] = act[j] && k[j] < kWalkKeyLimit;
                 cm[j] = CM && (cw & 1u);
                 pos[j] = cm[j] ? N.crow0 + mul24(tt, N.gk) + gk[j] : mul24(mul24(tt, N.n_ipc) + ca[j], N.gk) + gk[j];
@@ -1014,7 +1020,15 @@ PG_HD void classify_node_q(const DevTableSet& T, const DevNode& N, const L& img,
     PG_UNROLL
     for (int j = 0; j < Q; j++) cs[j] = ipc[j], cd[j] = ipc[Q + j];
     bool hooked = false;
-    const NodeEval<L, Q, H, CM, NP || UNI, UNI> ev{T, N, img, s, d, key, kack, cs, cd, gs, ga, hook, &hooked};
+    W2 mks[Q], mkd[Q];  // UNI: the common-row masks of the two classes, read once per tuple
+    if constexpr (UNI && CM) {
+        PG_UNROLL
+        for (int j = 0; j < Q; j++) {
+            mks[j] = img.u2(N.cmap + 2u * cs[j]);
+            mkd[j] = MODE == 2 ? img.u2(N.cmap + 2u * cd[j]) : mks[j];
+        }
+    }
+    const NodeEval<L, Q, H, CM, NP || UNI, UNI> ev{T, N, img, s, d, key, kack, cs, cd, gs, ga, hook, &hooked, &mks, &mkd};
     if (MODE == 1) {
         int32_t t[Q];
         bool run[Q];

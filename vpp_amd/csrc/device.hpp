@@ -90,10 +90,11 @@ struct DevNode {
     // (record word p of the cross numbering is image word p - rec0 + lrec); launches that do not
     // stage that part of the image clear lrec and read the cross array
     uint32_t rec0, lrec;
-    // uniform layout (every table covered, none in PAIR form; Tuning::node_uniform): table t's
-    // cross rows are over the node key classes, entry (t, ip class g, key class k) at word
-    // (t * n_ipc + g) * gk + k, and its common row (when cmap != 0) at image word crow0 + t * gk;
-    // tabinfo and kmap are not read
+    // uniform layout (every table covered, none in PAIR form, at most 64 tables;
+    // Tuning::node_uniform): table t's cross rows are over the node key classes, entry (t, ip
+    // class g, key class k) at word (t * n_ipc + g) * gk + k, and its common row (when cmap != 0)
+    // at image word crow0 + t * gk; tabinfo and kmap are not read, and the common-row marks at
+    // cmap are one uint2 mask per IP class (bit t: that class's row of table t is the common one)
     uint32_t uniform, crow0;
 };
 

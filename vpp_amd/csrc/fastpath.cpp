@@ -862,6 +862,9 @@ void build_common_rows(HostTableSet& h, const std::vector<uint32_t>& cov, const 
     if (!tu.node_common || bits > kCommonMapMaxBits) return;
     const std::vector<uint32_t>& X = h.node_cross;
     std::vector<uint32_t> sec, map((size_t)(bits / 32), 0);
+    // uniform layout: the marks as one 64-bit mask per IP class (uint2 {tables 0-31, 32-63}), so a
+    // connection reads its two classes' masks once instead of one bitmap word per evaluation
+    std::vector<uint32_t> masks(uni ? 2 * (size_t)G : 0, 0);
     std::vector<uint32_t> crow(T, 0);
     for (uint32_t t : cov) {
         const uint32_t base = img[N.tabinfo + 4 * t], nk = uni ? N.gk : an[t]->nkc;
@@ -882,15 +885,20 @@ void build_common_rows(HostTableSet& h, const std::vector<uint32_t>& cov, const 
         crow[t] = (uint32_t)sec.size();
         sec.insert(sec.end(), row(best), row(best) + nk);
         for (uint32_t g = 0; g < G; g++)
-            if (std::equal(row(g), row(g) + nk, row(best))) map[((size_t)t << rs) + (g >> 5)] |= 1u << (g & 31u);
+            if (std::equal(row(g), row(g) + nk, row(best))) {
+                if (uni) masks[2 * (size_t)g + (t >> 5)] |= 1u << (t & 31u);
+                else map[((size_t)t << rs) + (g >> 5)] |= 1u << (g & 31u);
+            }
     }
     while (sec.size() % 4) sec.push_back(0);
     const uint32_t s0 = (uint32_t)img.size();
     for (uint32_t t : cov) img[N.tabinfo + 4 * t + 2] = s0 + crow[t];
     img.insert(img.end(), sec.begin(), sec.end());
+    while (img.size() % 2) img.push_back(0);
     N.cmap = (uint32_t)img.size();
-    N.cmap_shift = rs;
-    img.insert(img.end(), map.begin(), map.end());
+    N.cmap_shift = uni ? 0u : rs;
+    if (uni) img.insert(img.end(), masks.begin(), masks.end());
+    else img.insert(img.end(), map.begin(), map.end());
     while (img.size() % 4) img.push_back(0);
     N.img_words = (uint32_t)img.size();
 }
@@ -993,7 +1001,8 @@ bool build_node(HostTableSet& h, const std::vector<TableAnalysis*>& an, const st
     // uniform layout (DevNode uniform): every table covered, none in PAIR form -- rows over the
     // node key classes at cross[(t * G + ip class) * GK + key class], so an evaluation computes
     // its entry's address from (t, classes) instead of reading tabinfo and kmap
-    const bool uni = tu.node_uniform && C == T && PC == 0 && (uint64_t)T * G < (1u << 24) &&
+    // (at most 64 tables: the common-row marks are then one 64-bit mask per IP class)
+    const bool uni = tu.node_uniform && C == T && PC == 0 && T <= 64 && (uint64_t)T * G < (1u << 24) &&
                      (uint64_t)T * G * GK <= kNodeCrossBudget;
     if (uni) entries = (uint64_t)T * G * GK;
 
