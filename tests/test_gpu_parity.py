@@ -304,6 +304,40 @@ def test_cluster_configs_gpu_vs_oracle(config):
     assert len(np.unique(got >> 30)) >= 2
 
 
+@pytest.mark.parametrize("any_pct", [0.05, 1.0])
+def test_conn_any_protocol_packets_deferred(any_pct):
+    """CONN over the uniform node (config 5's topology) classifies ANY-protocol packets (proto
+    codes > 2: evalACL skips the L4 test) after its main loop through the per-table path
+    (device.hip PG_CONN_DEFER_ANY): verdicts and the per-evaluation counters equal the oracle,
+    for a few such packets and for a batch of nothing else, ragged tail included."""
+    from oracle.world import World
+    from vpp_amd import workloads as W
+    w = W.config5(0, n_tuples=(1 << 18) + 7)
+    e = w.engine
+    assert e.node_stats()["uniform"]
+    b0 = D.TupleBatch(w.n_tuples, with_sport=True)
+    D.gen_tuples(e, b0, **w.gen)
+    src, dst, sport, dport, proto = b0.numpy(b0.n)
+    rng = np.random.default_rng(11)
+    m = rng.random(b0.n) < any_pct
+    proto = proto.copy()
+    proto[m] = rng.choice(np.array([3, 7, 255], np.uint8), int(m.sum()))
+    b = D.TupleBatch.from_numpy(src, dst, sport, dport, proto)
+    out = torch.empty(b.n, dtype=torch.int32, device="cuda")
+    cnt = torch.zeros(e.num_counter_slots(), dtype=torch.int64, device="cuda")
+    D.classify(e, MODE_CONN, -1, b, out, counters=cnt)
+    out0 = torch.empty(b.n, dtype=torch.int32, device="cuda")
+    D.classify(e, MODE_CONN, -1, b, out0)
+    torch.cuda.synchronize()
+    got = out.cpu().numpy().view(np.uint32)
+    assert np.array_equal(out0.cpu().numpy().view(np.uint32), got)
+    act, slot, hist = World(e, w.local_ifs, w.node_if).conn(src, dst, sport, dport, proto, threads=16, hist=True)
+    assert ((got >> 30) == act.astype(np.uint32)).all(), np.nonzero((got >> 30) != act)[0][:10]
+    assert ((got & 0x3FFFFFFF) == slot).all()
+    c = cnt.cpu().numpy()
+    assert np.array_equal(c, hist), np.nonzero(c != hist)[0][:10]
+
+
 @pytest.mark.parametrize("mode", [MODE_PERPOD, MODE_CONN])
 def test_k8s_object_cluster_gpu_vs_oracle(mode):
     """The cluster given as K8s objects (policy cache -> processor -> configurator -> renderer,

@@ -609,7 +609,9 @@ struct NoHook {
 // (table, IP class) row is the table's common row read it from the image, not the cross table.
 // NP: the node set has no PAIR tables (the launcher's build for it: no PAIR code at all)
 // UNI: the node's uniform cross layout (DevNode uniform; implies NP): entry addresses computed
-template <class L, int Q, class H = NoHook, bool CM = false, bool NP = false, bool UNI = false>
+// NOFB: no lane ever needs the per-table path (the caller deferred every ANY-protocol packet
+// and the node covers every table): its code is left out
+template <class L, int Q, class H = NoHook, bool CM = false, bool NP = false, bool UNI = false, bool NOFB = false>
 struct NodeEval {
     const DevTableSet& T;
     const DevNode& N;
@@ -764,6 +766,7 @@ struct NodeEval {
 #if defined(PG_PROBE_NOFB)  // measurement build only: the per-table fallback compiled out
         anyfb = false;
 #endif
+        if (NOFB) anyfb = false;
         if (anyfb) {
 #if PG_NODE_FB_CALL
             for (int j = 0; j < Q; j++)
@@ -815,27 +818,30 @@ PG_HD void eval_step(const DevTableSet& T, const EV& ev, const int32_t (&t)[Q], 
 
 // testConnection (aclengine_mock.go:424-501) of Q connections on resolved end points, each
 // of its up-to-4 evalACL steps in lockstep over the Q connections.
+// dfr (optional): connections deferred by the caller -- no evaluation and no count here (the
+// device's CONN node build classifies ANY-protocol packets after its main loop, device.hip)
 template <int Q, bool COUNT, class EV, class HS>
 PG_HD void conn_q(const DevTableSet& T, const EV& ev, const End (&es)[Q], const End (&ed)[Q], const HS& h,
-                  uint32_t (&out)[Q]) {
+                  uint32_t (&out)[Q], const bool* dfr = nullptr) {
     bool live[Q], srefl[Q], drefl[Q], same[Q], run[Q];
     uint32_t w[Q];
     int32_t t[Q];
     PG_UNROLL
     for (int j = 0; j < Q; j++) {
+        const bool df = dfr && dfr[j];
         // both interfaces resolved, and a pair the reference has a Connection* call for: the
         // end-point kinds (device.hpp kEndRemote / kEndInet) add to less than 3 -- remote pod <->
         // non-pod and non-pod <-> non-pod fail before any evaluation (aclengine_mock.go:343-347,
         // 388-392). Interfaces keep their kind bits, so "same interface" (srcIfName == dstIfName)
         // holds for remote <-> remote, both through the node-output interface.
-        live[j] = es[j].ifc >= 0 && ed[j].ifc >= 0 &&
+        live[j] = !df && es[j].ifc >= 0 && ed[j].ifc >= 0 &&
                   ((uint32_t)es[j].ifc >> kEndKindShift) + ((uint32_t)ed[j].ifc >> kEndKindShift) < 3u;
         srefl[j] = drefl[j] = false;
         same[j] = es[j].ifc == ed[j].ifc;
         w[j] = 0;
         if (!live[j]) {
             out[j] = verdict(3u, T.slot_unresolved);
-            if (COUNT) h.inc_cold(T.slot_unresolved);
+            if (COUNT && !df) h.inc_cold(T.slot_unresolved);
         }
     }
     // SYN: src interface inbound
@@ -896,12 +902,54 @@ PG_HD void conn_q(const DevTableSet& T, const EV& ev, const End (&es)[Q], const 
     }
 }
 
+// evalACL of ANY-protocol packets (the L4 test skipped, aclengine_mock.go:562): the first rule
+// whose src and dst match, with its ANY action (engine.cpp compile_acl_rule) -- eval_linear's
+// ANY branch, inline: the CONN node build's deferred pass calls nothing (a call anywhere in a
+// kernel costs its whole SGPR allocation)
+template <int Q>
+struct AnyEval {
+    const DevTableSet& T;
+    const uint32_t (&src)[Q];
+    const uint32_t (&dst)[Q];
+    PG_HD void operator()(const int32_t (&t)[Q], const bool (&act)[Q], bool rev, uint32_t (&w)[Q]) const {
+        for (int j = 0; j < Q; j++) {
+            if (!act[j]) continue;
+            const DevTable tab = load_tab(T.tabs, t[j]);
+            const uint32_t a = rev ? dst[j] : src[j], b = rev ? src[j] : dst[j];
+            uint32_t v = tab.dflt;
+            for (uint32_t i = 0; i < tab.n_rules; i++) {
+                const DevRule r = T.rules[tab.rule_base + i];
+                if ((a & r.smask) == r.snet && (b & r.dmask) == r.dnet && (r.act >> 4) != kActNever) {
+                    v = verdict((r.act >> 4) & 3u, tab.rule_base + i);
+                    break;
+                }
+            }
+            w[j] = v;
+        }
+    }
+};
+
+// testConnection of one ANY-protocol connection through the iphash and AnyEval (the CONN node
+// build's deferred pass, device.hip PG_CONN_DEFER_ANY)
+template <bool COUNT, class HS>
+PG_HD uint32_t conn_any_1(const DevTableSet& T, uint32_t s, uint32_t d, const HS& h) {
+    const uint32_t ips[2] = {s, d};
+    End e[2];
+    probe_q(T, ips, e);
+    const End es[1] = {e[0]}, ed[1] = {e[1]};
+    const uint32_t s1[1] = {s}, d1[1] = {d};
+    const AnyEval<1> ev{T, s1, d1};
+    uint32_t o[1];
+    conn_q<1, COUNT>(T, ev, es, ed, h, o);
+    return o[0];
+}
+
 // Q tuples of one lane, any mode, per-table path. SINGLE: tab0 is the (uniform) table, its
 // blob at `blobs`.
-template <int MODE, bool COUNT, int Q, bool PRED = false>
+template <int MODE, bool COUNT, int Q, bool PRED = false, class HS = Hist>
 PG_HD void classify_q(const DevTableSet& T, const uint32_t* blobs, const DevTable& tab0, const uint32_t (&s)[Q],
                       const uint32_t (&d)[Q], const uint32_t (&sp)[Q], const uint32_t (&dp)[Q],
-                      const uint32_t (&pr)[Q], const Hist& h, uint32_t (&out)[Q], const uint32_t* rootb = nullptr) {
+                      const uint32_t (&pr)[Q], const HS& h, uint32_t (&out)[Q], const uint32_t* rootb = nullptr) {
     uint32_t key[Q], kack[Q];
     PG_UNROLL
     for (int j = 0; j < Q; j++) key[j] = pkt_key(pr[j], dp[j]), kack[j] = pkt_key(pr[j], sp[j]);
@@ -948,8 +996,11 @@ PG_HD void classify_q(const DevTableSet& T, const uint32_t* blobs, const DevTabl
 
 // Q tuples of one lane, PERPOD / CONN, node path. `img` reads the node image (LDS copy or
 // global memory).
+// DEFER (CONN over a uniform node, every table covered): ANY-protocol packets (the only ones
+// the node cannot classify) are left to the caller -- no evaluation, no count, a placeholder
+// verdict -- so the evaluation carries no per-table fallback (device.hip PG_CONN_DEFER_ANY)
 template <int MODE, bool COUNT, int Q, bool PRED = false, bool CM = false, bool NP = false, bool UNI = false,
-          class L, class HS, class H = NoHook>
+          bool DEFER = false, class L, class HS, class H = NoHook>
 PG_HD void classify_node_q(const DevTableSet& T, const DevNode& N, const L& img, const uint32_t (&s)[Q],
                            const uint32_t (&d)[Q], const uint32_t (&sp)[Q], const uint32_t (&dp)[Q],
                            const uint32_t (&pr)[Q], const HS& h, uint32_t (&out)[Q], const H& hook = H()) {
@@ -1028,7 +1079,8 @@ PG_HD void classify_node_q(const DevTableSet& T, const DevNode& N, const L& img,
             mkd[j] = MODE == 2 ? img.u2(N.cmap + 2u * cd[j]) : mks[j];
         }
     }
-    const NodeEval<L, Q, H, CM, NP || UNI, UNI> ev{T, N, img, s, d, key, kack, cs, cd, gs, ga, hook, &hooked, &mks, &mkd};
+    constexpr bool DF = DEFER && MODE == 2 && UNI;
+    const NodeEval<L, Q, H, CM, NP || UNI, UNI, DF> ev{T, N, img, s, d, key, kack, cs, cd, gs, ga, hook, &hooked, &mks, &mkd};
     if (MODE == 1) {
         int32_t t[Q];
         bool run[Q];
@@ -1047,7 +1099,14 @@ PG_HD void classify_node_q(const DevTableSet& T, const DevNode& N, const L& img,
         End es[Q], ed[Q];
         PG_UNROLL
         for (int j = 0; j < Q; j++) es[j] = node_end(img, N, cs[j]), ed[j] = node_end(img, N, cd[j]);
-        conn_q<Q, COUNT>(T, ev, es, ed, h, out);
+        if (DF) {
+            bool dfr[Q];
+            PG_UNROLL
+            for (int j = 0; j < Q; j++) dfr[j] = key[j] >= kWalkKeyLimit || kack[j] >= kWalkKeyLimit;
+            conn_q<Q, COUNT>(T, ev, es, ed, h, out, dfr);
+        } else {
+            conn_q<Q, COUNT>(T, ev, es, ed, h, out);
+        }
     }
     if (!hooked) hook();  // no evaluation ran in this lane
 }

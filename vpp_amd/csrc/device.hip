@@ -451,6 +451,15 @@ constexpr size_t kLdsPerCU = 160u << 10;
 #ifndef PG_NODE_FULLH  // node kernels whose LDS histogram holds every slot: the specialised build (STAGE + 16)
 #define PG_NODE_FULLH 1
 #endif
+// CONN over a uniform node (STAGE + 96): ANY-protocol packets, the only ones the node cannot
+// classify, are deferred to a pass after the main loop (the per-table path, counted into the
+// same histogram), so the loop carries no per-table fallback. The out-of-line fallback call
+// in the loop cost the whole kernel its SGPR allocation: 54 SGPRs spilled to VGPR lanes, a
+// v_readlane per use (A/B on MI355X, a build without the fallback: config 5 with counters
+// 123 -> 139 Gpps, without 152 -> 167.5; PERPOD unchanged, so it keeps the call)
+#ifndef PG_CONN_DEFER_ANY
+#define PG_CONN_DEFER_ANY 1
+#endif
 #ifndef PG_TPL  // tuples per lane per loop iteration (4 or 8)
 #define PG_TPL 4
 #endif
@@ -510,12 +519,9 @@ __device__ __forceinline__ void st_words(const Words<NW>& v, uint32_t* p) {
 #ifndef PG_SINGLE_HBM_WPE  // (A/B on MI355X, config 4: 8 = 164.6 Gpps with 2 spills, 1 = 175.7)
 #define PG_SINGLE_HBM_WPE 1
 #endif
-template <int MODE, bool COUNT, bool NODE, int STAGE = 1>
-constexpr int kernel_wpe() {
-    return !NODE ? (MODE == 0 && ((STAGE & 7) == 0 || (STAGE & 7) == 2) ? PG_SINGLE_HBM_WPE : 1)
-                 : ((MODE == 2 && (COUNT || PG_CONN_WPE8_ALL)) || (MODE == 1 && COUNT && (STAGE & 16) && PG_POD_FULLH_WPE8)
-                        ? PG_CONN_COUNT_WPE : PG_NODE_WPE);
-}
+#ifndef PG_NODE_WIDE_BS  // workgroup size of the wide node builds (node_wide)
+#define PG_NODE_WIDE_BS 1024
+#endif
 // node builds at 64 registers (wpe 8): 1024-thread workgroups and no stream prefetch (its
 // registers): CONN, and PERPOD counting into an LDS histogram of every slot (image + histogram
 // leave LDS for two workgroups per CU: 16 waves at 512 threads, 32 at 1024; A/B on MI355X,
@@ -523,7 +529,12 @@ constexpr int kernel_wpe() {
 // prefetching 512-thread build stays ahead: config 3 317 vs 301, config 6 with counters 147 vs 142)
 template <int MODE, bool COUNT, bool NODE, int STAGE = 1>
 constexpr bool node_wide() {
-    return NODE && kernel_wpe<MODE, COUNT, NODE, STAGE>() >= 8;
+    return NODE && ((MODE == 2 && (COUNT || PG_CONN_WPE8_ALL)) || (MODE == 1 && COUNT && (STAGE & 16) && PG_POD_FULLH_WPE8));
+}
+template <int MODE, bool COUNT, bool NODE, int STAGE = 1>
+constexpr int kernel_wpe() {
+    return !NODE ? (MODE == 0 && ((STAGE & 7) == 0 || (STAGE & 7) == 2) ? PG_SINGLE_HBM_WPE : 1)
+                 : (node_wide<MODE, COUNT, NODE, STAGE>() ? PG_CONN_COUNT_WPE : PG_NODE_WPE);
 }
 // STAGE_ + 8 (SINGLE, STAGE 0-2): the table is dst-free (kFlagDstFree: no rule tests dst), so
 // the dst stream is not read
@@ -545,6 +556,9 @@ void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
     constexpr bool NOPAIR = NODE && (STAGE_ & 32);
     // STAGE_ + 64 (node kernels): the node's uniform cross layout (DevNode uniform; with + 32)
     constexpr bool UNIF = NODE && NOPAIR && (STAGE_ & 64);
+    // CONN over a uniform node: ANY-protocol packets deferred past the main loop (PG_CONN_DEFER_ANY)
+    constexpr bool DEFER = UNIF && MODE == 2 && PG_CONN_DEFER_ANY;
+    bool saw_any = false;  // (DEFER) this lane deferred a packet
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     uint32_t* hist = smem + (STAGE ? stage_words : 0u);
     // node kernels: the LDS histogram, when used, holds every slot (HistT<true>: no window test)
@@ -678,6 +692,7 @@ void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
             dpv[j] = (g.dp.w[j / 2] >> (16 * (j & 1))) & 0xFFFFu;
             spv[j] = (g.sp.w[j / 2] >> (16 * (j & 1))) & 0xFFFFu;
             prv[j] = (g.pr.w[j / 4] >> (8 * (j & 3))) & 0xFFu;
+            if (DEFER) saw_any |= prv[j] > 2u;
         }
 #if PG_PROBE_STREAM
         for (int j = 0; j < P; j++) o[j] = sv[j] ^ dv[j] ^ dpv[j] ^ prv[j] ^ spv[j];
@@ -703,9 +718,9 @@ void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
                 classify_candi_q<COUNT, QC>(T, LdsLoader{}, DevLoader{T.blobs + tab0.blob_off}, tab0, cs, cdp, cpr, h, co);
             } else if constexpr (NODE) {
                 if (c == (PG_HOOK_LAST ? P - QC : 0))
-                    classify_node_q<MODE, COUNT, QC, STAGE && PG_PRED, STAGE == 3, NOPAIR, UNIF>(T, T.node, img, cs, cd, csp, cdp, cpr, h, co, hk);
+                    classify_node_q<MODE, COUNT, QC, STAGE && PG_PRED, STAGE == 3, NOPAIR, UNIF, DEFER>(T, T.node, img, cs, cd, csp, cdp, cpr, h, co, hk);
                 else
-                    classify_node_q<MODE, COUNT, QC, STAGE && PG_PRED, STAGE == 3, NOPAIR, UNIF>(T, T.node, img, cs, cd, csp, cdp, cpr, h, co);
+                    classify_node_q<MODE, COUNT, QC, STAGE && PG_PRED, STAGE == 3, NOPAIR, UNIF, DEFER>(T, T.node, img, cs, cd, csp, cdp, cpr, h, co);
             } else {
                 classify_q<MODE, COUNT, QC, STAGE == 1 && PG_PRED>(T, blobs, tab0, cs, cd, csp, cdp, cpr, h, co, rootb);
             }
@@ -749,9 +764,25 @@ void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
         else if constexpr (FD) classify_fd_q<COUNT, 1>(T, LdsLoader{}, DevLoader{fd_blob}, tab0, s1, dp1, pr1, h, o);
         else if constexpr (MODE == 0 && STAGE == 6)
             classify_candi_q<COUNT, 1>(T, LdsLoader{}, DevLoader{T.blobs + tab0.blob_off}, tab0, s1, dp1, pr1, h, o);
-        else if constexpr (NODE) classify_node_q<MODE, COUNT, 1, STAGE && PG_PRED, STAGE == 3, NOPAIR, UNIF>(T, T.node, img, s1, d1, sp1, dp1, pr1, h, o);
+        else if constexpr (NODE) classify_node_q<MODE, COUNT, 1, STAGE && PG_PRED, STAGE == 3, NOPAIR, UNIF, DEFER>(T, T.node, img, s1, d1, sp1, dp1, pr1, h, o);
         else classify_q<MODE, COUNT, 1, STAGE == 1 && PG_PRED>(T, blobs, tab0, s1, d1, sp1, dp1, pr1, h, o, rootb);
         out[i] = o[0];
+        if (DEFER) saw_any |= pr1[0] > 2u;
+    }
+    if constexpr (DEFER) {
+        // the packets deferred above (ANY protocol: rare): testConnection with the iphash end
+        // points and the ANY-protocol first match, inline (conn_any_1), counted into the same
+        // histogram; the lane replays its own tuple sequence reading only the protocol stream
+        if (saw_any) {
+            auto one = [&](uint64_t i) { out[i] = conn_any_1<COUNT>(T, src[i], dst[i], h); };
+            for (uint64_t qq = first; qq < nfull; qq += stride) {
+                const Words<P / 4> pw = ld_words<P / 4>(reinterpret_cast<const uint32_t*>(proto + qq * P));
+                for (int j = 0; j < P; j++)
+                    if (((pw.w[j / 4] >> (8 * (j & 3))) & 0xFFu) > 2u) one(qq * P + j);
+            }
+            for (uint64_t i = nfull * P + first; i < n; i += stride)
+                if (proto[i] > 2u) one(i);
+        }
     }
     if (COUNT) {
         h.flush_hot();
@@ -1000,6 +1031,11 @@ static void launch_one(const DevTableSet& T, const Tuning& tu, int t, const uint
         // image copy then serves 16 waves (A/B on MI355X, the 10k-rule sweep table, 59.5 KB:
         // 393.8 -> 471.5 Gpps; config 2's 49 KB blob, three fit: 530 vs 475 at 1024)
         const size_t lds_bytes = hist + (size_t)stage * 4;
+        if constexpr (node_wide<MODE, COUNT, NODE, STAGE>() && PG_NODE_WIDE_BS != 1024)
+            if (!tu.block_stage)
+                return launch_bs<MODE, COUNT, VEC, STAGE, NODE, PG_NODE_WIDE_BS>(T, tu, t, src, dst, sport, dport, proto,
+                                                                                n, out, counters, st, hist, cells, stage,
+                                                                                items);
         const uint32_t bs = tu.block_stage ? tu.block_stage
                             : node_wide<MODE, COUNT, NODE, STAGE>()                                ? 1024u
                             : (MODE == 0 && (STAGE & 7) == 4 && lds_bytes > kLdsPerCU / 3 && PG_FD_BS1024) ? 1024u
