@@ -43,19 +43,29 @@ constexpr uint32_t kLeaf = 0x80000000u;
 constexpr uint32_t kTrieStrideShift = 26u, kTrieChildMask = (1u << kTrieStrideShift) - 1u;
 PG_HD uint32_t trie_child(uint32_t e) { return e & kTrieChildMask; }
 PG_HD uint32_t trie_stride(uint32_t e) { return (e >> kTrieStrideShift) & 31u; }
-// Node-image tries (LDS-staged): non-leaf entry = child byte offset << 5 | stride of the child
-// level. The node tries take uniform strides below the root (min(8, bits left), fastpath.cpp
-// build_node), so the bit offset of a level's index is the same for every entry -- a per-level
-// constant the walk keeps in a scalar register (node_next_shift). The child entry of address a
-// is at byte
-//   (e >> 5) + 4 * ((a >> shift) & ((1 << (e & 31)) - 1))
-// -- on the device one v_bfe_u32 (its width operand is e itself: the hardware reads only the
-// low 5 bits), one v_lshl_add_u32 and, off the dependency chain, one shift of e.
-constexpr uint32_t kNodeChildMaxWords = 1u << 25;  // 128 MiB of image
+// Node-image tries (LDS-staged). The node tries take uniform strides below the root (min(8,
+// bits left)), so the bit offset of a level's index is the same for every entry -- a per-level
+// constant the walk keeps in a scalar register (node_next_shift). A leaf points at its
+// class's record (DevNode) with stride 0: a record a leaf above the last level points at holds
+// that leaf's value in its first word, so a finished lookup re-reads it and every lookup takes
+// exactly the trie's depth in reads. Two encodings:
+//  * aligned (the uniform node layout; fastpath.cpp build_trie kEncNodeA): an entry is a byte
+//    address. The builder places every child table at an address congruent to its stride mod
+//    32 (strides below the root are then 8 or 4: the root stride is a multiple of 4), so the
+//    entry's low 5 bits are the stride, and a leaf above the last level points at a record on a
+//    32-byte boundary. The child entry of address a is at byte
+//      e + 4 * ((a >> shift) & ((1 << (e & 31)) - 1))
+//    -- on the device one v_bfe_u32 (its width operand is e itself: the hardware reads only the
+//    low 5 bits) and one v_lshl_add_u32.
+//  * shifted (kEncNode): entry = byte address << 5 | stride, any strides: one shift of e more.
+constexpr uint32_t kNodeChildMaxWords = 1u << 25;  // 128 MiB of image (shifted byte addresses in 32 bits)
 constexpr uint32_t kNodeStride = 8;  // stride of the levels below the root
-PG_HD constexpr uint32_t node_entry(uint32_t child_words, uint32_t stride) { return (child_words * 4u) << 5 | stride; }
+PG_HD constexpr uint32_t node_entry(uint32_t child_words, uint32_t stride, bool aligned) {
+    return aligned ? child_words * 4u : (child_words * 4u) << 5 | stride;
+}
 // bits below the next level, given the bits below the current one (uniform per level)
 PG_HD uint32_t node_next_shift(uint32_t rem) { return rem - (rem < kNodeStride ? rem : kNodeStride); }
+template <bool ALIGNED>
 PG_HD uint32_t node_child_byte(uint32_t e, uint32_t a, uint32_t shift) {
 #if defined(__HIP_DEVICE_COMPILE__)
     const uint32_t idx = __builtin_amdgcn_ubfe(a, shift, e);
@@ -63,8 +73,14 @@ PG_HD uint32_t node_child_byte(uint32_t e, uint32_t a, uint32_t shift) {
     const uint32_t w = e & 31u;
     const uint32_t idx = shift >= 32u ? 0u : (a >> shift) & (w >= 32u ? 0xFFFFFFFFu : ((1u << w) - 1u));
 #endif
-    return (e >> 5) + (idx << 2);
+    return (ALIGNED ? e : e >> 5) + (idx << 2);
 }
+// node class records (DevNode), log2 bytes: the uniform layout (aligned tries, A) IPv4 16 B
+// and key 32 B; otherwise 4-B self words
+template <bool A>
+PG_HD constexpr uint32_t node_ip_rec_shift() { return A ? 4u : 2u; }
+template <bool A>
+PG_HD constexpr uint32_t node_key_rec_shift() { return A ? 5u : 2u; }
 constexpr uint32_t kSrcRoot = 16u;       // the src trie root follows the 16-word blob header
 constexpr uint32_t kWalkKeyLimit = 0x30000u;  // keys >= this (ANY protocol) take the linear path
 // key bound of records that match every key: covers the whole 18-bit walk range, ANY keys

@@ -108,6 +108,9 @@ struct DevLoader {
         return W4{b[i], b[i + 1], b[i + 2], b[i + 3]};
 #endif
     }
+    // at byte addresses (8- / 16-byte aligned): node class records
+    PG_HD W2 u2_at_byte(uint32_t off) const { return u2(off / 4u); }
+    PG_HD W4 u4_at_byte(uint32_t off) const { return u4(off / 4u); }
 };
 
 // Loads from the kernel's LDS image, which starts at LDS address 0 (k_classify's dynamic shared
@@ -130,12 +133,22 @@ struct LdsLoader {
         const uint4 v = at<uint4>(i * 4u);
         return W4{v.x, v.y, v.z, v.w};
     }
+    PG_HD W2 u2_at_byte(uint32_t off) const {
+        const uint2 v = at<uint2>(off);
+        return W2{v.x, v.y};
+    }
+    PG_HD W4 u4_at_byte(uint32_t off) const {
+        const uint4 v = at<uint4>(off);
+        return W4{v.x, v.y, v.z, v.w};
+    }
 #else  // host builds never instantiate it (kernels only)
     uint32_t u32(uint32_t) const { return 0; }
     uint32_t at_byte(uint32_t) const { return 0; }
     uint32_t u16(uint32_t) const { return 0; }
     W2 u2(uint32_t) const { return W2{0, 0}; }
     W4 u4(uint32_t) const { return W4{0, 0, 0, 0}; }
+    W2 u2_at_byte(uint32_t) const { return W2{0, 0}; }
+    W4 u4_at_byte(uint32_t) const { return W4{0, 0, 0, 0}; }
 #endif
 };
 
@@ -532,30 +545,32 @@ struct TabEval {
 // table per evaluation, cross[tabinfo[t].base + ipclass * nkc_t + kmap[t][keyclass]]: a
 // verdict, or (kNodeList) the first of the dst records to test. Tables the node does not
 // cover, LINEAR tables and ANY-protocol packets take the per-table path.
-// Fixed-depth trie lookups (DevNode: leaves point at their class's self word, which points
-// at itself), in lockstep and without per-lane branches: the root read (stride s1 over a W-bit
-// address), then depth - 1 steps of one bit-field extract and one shifted add each (blobwalk.hpp
-// node_child_byte) at a per-level bit offset; the class is the self word's index (e >> 7). PRED
-// is unused (kept for the callers).
-template <bool PRED, class L, int Q>
-PG_HD void node_trie_q(const L& ld, uint32_t root, uint32_t s1, uint32_t W, uint32_t depth, uint32_t self0,
-                       const uint32_t (&a)[Q], uint32_t (&c)[Q]) {
-    uint32_t e[Q], rem = W - s1;
+// Fixed-depth trie lookups (DevNode: a leaf points at its class record; a record that a leaf
+// above the last level points at holds that leaf's value in its first word), in lockstep and
+// without per-lane branches: the root read (stride s1 over a W-bit address), then depth - 1
+// steps of one bit-field extract and one shifted add each (blobwalk.hpp node_child_byte, the
+// aligned encoding for the uniform layout, A) at a per-level bit offset. r: the record byte
+// addresses; the class is (r >> record shift) - self. PRED is unused (kept for the callers).
+template <bool PRED, bool A, class L, int Q>
+PG_HD void node_trie_q(const L& ld, uint32_t root, uint32_t s1, uint32_t W, uint32_t depth, const uint32_t (&a)[Q],
+                       uint32_t (&r)[Q]) {
+    uint32_t rem = W - s1;
     PG_UNROLL
-    for (int j = 0; j < Q; j++) e[j] = ld.u32(root + (a[j] >> (W - s1)));
+    for (int j = 0; j < Q; j++) r[j] = ld.u32(root + (a[j] >> (W - s1)));
     for (uint32_t l = 1; l < depth; l++) {
         rem = node_next_shift(rem);
         PG_UNROLL
-        for (int j = 0; j < Q; j++) e[j] = ld.at_byte(node_child_byte(e[j], a[j], rem));
+        for (int j = 0; j < Q; j++) r[j] = ld.at_byte(node_child_byte<A>(r[j], a[j], rem));
     }
     PG_UNROLL
-    for (int j = 0; j < Q; j++) c[j] = (e[j] >> 7) - self0;
+    for (int j = 0; j < Q; j++) r[j] = A ? r[j] : r[j] >> 5;
 }
 
 // The IPv4 trie (addresses a) and the L4-key trie (keys b) in one lockstep loop: independent
-// walks, so their dependent LDS reads overlap.
-template <bool PRED, class L, int QA, int QB>
-PG_HD void node_trie2_q(const L& ld, const DevNode& N, const uint32_t (&a)[QA], uint32_t (&ca)[QA],
+// walks, so their dependent LDS reads overlap. rr: the IPv4 class records' byte addresses; cb:
+// the key classes.
+template <bool PRED, bool A, class L, int QA, int QB>
+PG_HD void node_trie2_q(const L& ld, const DevNode& N, const uint32_t (&a)[QA], uint32_t (&rr)[QA],
                         const uint32_t (&b)[QB], uint32_t (&cb)[QB]) {
     uint32_t ea[QA], eb[QB], ra = 32u - N.ip_s1, rb = 18u - N.key_k1;
     PG_UNROLL
@@ -567,36 +582,44 @@ PG_HD void node_trie2_q(const L& ld, const DevNode& N, const uint32_t (&a)[QA], 
         ra = node_next_shift(ra);
         rb = node_next_shift(rb);
         PG_UNROLL
-        for (int j = 0; j < QA; j++) ea[j] = ld.at_byte(node_child_byte(ea[j], a[j], ra));
+        for (int j = 0; j < QA; j++) ea[j] = ld.at_byte(node_child_byte<A>(ea[j], a[j], ra));
         PG_UNROLL
-        for (int j = 0; j < QB; j++) eb[j] = ld.at_byte(node_child_byte(eb[j], b[j], rb));
+        for (int j = 0; j < QB; j++) eb[j] = ld.at_byte(node_child_byte<A>(eb[j], b[j], rb));
     }
     for (uint32_t l = dmin; l < N.ip_depth; l++) {
         ra = node_next_shift(ra);
         PG_UNROLL
-        for (int j = 0; j < QA; j++) ea[j] = ld.at_byte(node_child_byte(ea[j], a[j], ra));
+        for (int j = 0; j < QA; j++) ea[j] = ld.at_byte(node_child_byte<A>(ea[j], a[j], ra));
     }
     for (uint32_t l = dmin; l < N.key_depth; l++) {
         rb = node_next_shift(rb);
         PG_UNROLL
-        for (int j = 0; j < QB; j++) eb[j] = ld.at_byte(node_child_byte(eb[j], b[j], rb));
+        for (int j = 0; j < QB; j++) eb[j] = ld.at_byte(node_child_byte<A>(eb[j], b[j], rb));
     }
     PG_UNROLL
-    for (int j = 0; j < QA; j++) ca[j] = (ea[j] >> 7) - N.ipself;
+    for (int j = 0; j < QA; j++) rr[j] = A ? ea[j] : ea[j] >> 5;
     PG_UNROLL
-    for (int j = 0; j < QB; j++) cb[j] = (eb[j] >> 7) - N.kself;
+    for (int j = 0; j < QB; j++) cb[j] = (eb[j] >> (A ? node_key_rec_shift<A>() : node_key_rec_shift<A>() + 5)) - N.kself;
 }
 
 #ifndef PG_NODE_WALK2  // node kernels: IPv4 and key tries in one lockstep walk
 #define PG_NODE_WALK2 1
 #endif
 
-// end point of a node IP class (ipinfo: {interface, tin | tout << 16}, 0xFFFF = no ACL)
+// end point of a node IP class outside the uniform layout (ipinfo: {interface, tin | tout << 16},
+// 0xFFFF = no ACL); the uniform layout's class records pack it (node_end_packed)
 template <class L>
 PG_HD End node_end(const L& img, const DevNode& N, uint32_t ipc) {
     const W2 v = img.u2(N.ipinfo + 2u * ipc);
     const uint32_t tin = v.y & 0xFFFFu, tout = v.y >> 16;
     return End{(int32_t)v.x, tin == 0xFFFFu ? -1 : (int32_t)tin, tout == 0xFFFFu ? -1 : (int32_t)tout};
+}
+// packed end point (uniform layout: at most 64 tables): interface index (14 bits) | end-point kind
+// << 14 (0xFFFF: unresolved) | tin << 16 | tout << 24 (0xFF = no ACL)
+PG_HD End node_end_packed(uint32_t p) {
+    const uint32_t f = p & 0xFFFFu, tin = (p >> 16) & 0xFFu, tout = p >> 24;
+    return End{f == 0xFFFFu ? -1 : (int32_t)((f & 0x3FFFu) | ((f >> 14) << kEndKindShift)), tin == 0xFFu ? -1 : (int32_t)tin,
+               tout == 0xFFu ? -1 : (int32_t)tout};
 }
 
 struct NoHook {
@@ -1007,8 +1030,8 @@ PG_HD void classify_node_q(const DevTableSet& T, const DevNode& N, const L& img,
     uint32_t key[Q], kack[Q];
     PG_UNROLL
     for (int j = 0; j < Q; j++) key[j] = pkt_key(pr[j], dp[j]), kack[j] = MODE == 2 ? pkt_key(pr[j], sp[j]) : key[j];
-    // node IP classes of src and dst, node key classes of both keys: 2Q + 2Q trie walks
-    uint32_t ips[2 * Q], ipc[2 * Q];
+    // node IP class records of src and dst, node key classes of both keys: 2Q + 2Q trie walks
+    uint32_t ips[2 * Q], rec[2 * Q];
     PG_UNROLL
     for (int j = 0; j < Q; j++) ips[j] = s[j], ips[Q + j] = d[j];
     uint32_t cs[Q], cd[Q], gs[Q], ga[Q];
@@ -1020,7 +1043,7 @@ PG_HD void classify_node_q(const DevTableSet& T, const DevNode& N, const L& img,
             keys[j] = key[j] < kWalkKeyLimit ? key[j] : 0u;
             keys[Q + j] = kack[j] < kWalkKeyLimit ? kack[j] : 0u;
         }
-        node_trie2_q<PRED>(img, N, ips, ipc, keys, kc);
+        node_trie2_q<PRED, UNI>(img, N, ips, rec, keys, kc);
         PG_UNROLL
         for (int j = 0; j < Q; j++) gs[j] = kc[j], ga[j] = kc[Q + j];
     } else {
@@ -1029,15 +1052,15 @@ PG_HD void classify_node_q(const DevTableSet& T, const DevNode& N, const L& img,
         for (int j = 0; j < Q; j++) keys[j] = key[j] < kWalkKeyLimit ? key[j] : 0u;
 #if defined(PG_PROBE_NODSTWALK)  // measurement build only: PERPOD walks src only (dst class = src's)
         {
-            uint32_t sa[Q], sc[Q];
+            uint32_t sa[Q], sr[Q];
             PG_UNROLL
             for (int j = 0; j < Q; j++) sa[j] = ips[j];
-            node_trie2_q<PRED>(img, N, sa, sc, keys, gs);
+            node_trie2_q<PRED, UNI>(img, N, sa, sr, keys, gs);
             PG_UNROLL
-            for (int j = 0; j < Q; j++) ipc[j] = sc[j], ipc[Q + j] = sc[j];
+            for (int j = 0; j < Q; j++) rec[j] = sr[j], rec[Q + j] = sr[j];
         }
 #else
-        node_trie2_q<PRED>(img, N, ips, ipc, keys, gs);
+        node_trie2_q<PRED, UNI>(img, N, ips, rec, keys, gs);
 #endif
         PG_UNROLL
         for (int j = 0; j < Q; j++) ga[j] = gs[j];
@@ -1045,38 +1068,48 @@ PG_HD void classify_node_q(const DevTableSet& T, const DevNode& N, const L& img,
 #else
 #if defined(PG_PROBE_NOWALK)  // measurement build only: IP classes without the trie walk
     PG_UNROLL
-    for (int j = 0; j < 2 * Q; j++) ipc[j] = ips[j] % N.n_ipc;
+    for (int j = 0; j < 2 * Q; j++) rec[j] = (ips[j] % N.n_ipc + N.ipself) << node_ip_rec_shift<UNI>();
 #else
-    node_trie_q<PRED>(img, 0u, N.ip_s1, 32u, N.ip_depth, N.ipself, ips, ipc);
+    node_trie_q<PRED, UNI>(img, 0u, N.ip_s1, 32u, N.ip_depth, ips, rec);
 #endif
-    if (MODE == 2) {
-        uint32_t keys[2 * Q], kc[2 * Q];
+    {
+        const uint32_t nk = MODE == 2 ? 2 * Q : Q;
+        uint32_t keys[2 * Q], kr[2 * Q];
         PG_UNROLL
         for (int j = 0; j < Q; j++) {
             keys[j] = key[j] < kWalkKeyLimit ? key[j] : 0u;
             keys[Q + j] = kack[j] < kWalkKeyLimit ? kack[j] : 0u;
         }
-        node_trie_q<PRED>(img, N.key_root, N.key_k1, 18u, N.key_depth, N.kself, keys, kc);
-        PG_UNROLL
-        for (int j = 0; j < Q; j++) gs[j] = kc[j], ga[j] = kc[Q + j];
-    } else {
-        uint32_t keys[Q];
-        PG_UNROLL
-        for (int j = 0; j < Q; j++) keys[j] = key[j] < kWalkKeyLimit ? key[j] : 0u;
-        node_trie_q<PRED>(img, N.key_root, N.key_k1, 18u, N.key_depth, N.kself, keys, gs);
-        PG_UNROLL
-        for (int j = 0; j < Q; j++) ga[j] = gs[j];
-    }
-#endif
-    PG_UNROLL
-    for (int j = 0; j < Q; j++) cs[j] = ipc[j], cd[j] = ipc[Q + j];
-    bool hooked = false;
-    W2 mks[Q], mkd[Q];  // UNI: the common-row masks of the two classes, read once per tuple
-    if constexpr (UNI && CM) {
+        node_trie_q<PRED, UNI>(img, N.key_root, N.key_k1, 18u, N.key_depth, keys, kr);
         PG_UNROLL
         for (int j = 0; j < Q; j++) {
-            mks[j] = img.u2(N.cmap + 2u * cs[j]);
-            mkd[j] = MODE == 2 ? img.u2(N.cmap + 2u * cd[j]) : mks[j];
+            gs[j] = (kr[j] >> node_key_rec_shift<UNI>()) - N.kself;
+            ga[j] = nk > (uint32_t)Q ? (kr[Q + j] >> node_key_rec_shift<UNI>()) - N.kself : gs[j];
+        }
+    }
+#endif
+    // the class numbers (cross-array rows): records from record ipself on
+    constexpr uint32_t RS = node_ip_rec_shift<UNI>();
+    PG_UNROLL
+    for (int j = 0; j < Q; j++) cs[j] = (rec[j] >> RS) - N.ipself, cd[j] = (rec[Q + j] >> RS) - N.ipself;
+    bool hooked = false;
+    W2 mks[Q], mkd[Q];  // UNI: the common-row masks of the two classes, read once per tuple
+    End es[Q], ed[Q];   // CONN: both end points; PERPOD: ed
+    PG_UNROLL
+    for (int j = 0; j < Q; j++) {
+        if constexpr (UNI) {  // record {self, packed end point, mask lo, mask hi}
+            if (MODE == 2) {
+                const W4 rs = img.u4_at_byte(rec[j]), rd = img.u4_at_byte(rec[Q + j]);
+                es[j] = node_end_packed(rs.y), ed[j] = node_end_packed(rd.y);
+                mks[j] = W2{rs.z, rs.w}, mkd[j] = W2{rd.z, rd.w};
+            } else {
+                ed[j] = node_end_packed(img.at_byte(rec[Q + j] + 4u));
+                mks[j] = CM ? img.u2_at_byte(rec[j] + 8u) : W2{0u, 0u};
+                mkd[j] = mks[j];
+            }
+        } else {  // self words; ipinfo {interface, tin | tout << 16} per class
+            if (MODE == 2) es[j] = node_end(img, N, cs[j]);
+            ed[j] = node_end(img, N, cd[j]);
         }
     }
     constexpr bool DF = DEFER && MODE == 2 && UNI;
@@ -1086,9 +1119,8 @@ PG_HD void classify_node_q(const DevTableSet& T, const DevNode& N, const L& img,
         bool run[Q];
         PG_UNROLL
         for (int j = 0; j < Q; j++) {
-            const End e = node_end(img, N, cd[j]);
-            run[j] = e.ifc >= 0;
-            t[j] = e.tout;
+            run[j] = ed[j].ifc >= 0;
+            t[j] = ed[j].tout;
             if (!run[j]) {
                 out[j] = verdict(kActFailure, T.slot_unresolved);
                 if (COUNT) h.inc_cold(T.slot_unresolved);
@@ -1096,9 +1128,6 @@ PG_HD void classify_node_q(const DevTableSet& T, const DevNode& N, const L& img,
         }
         eval_step<Q, COUNT>(T, ev, t, run, false, h, out);
     } else {
-        End es[Q], ed[Q];
-        PG_UNROLL
-        for (int j = 0; j < Q; j++) es[j] = node_end(img, N, cs[j]), ed[j] = node_end(img, N, cd[j]);
         if (DF) {
             bool dfr[Q];
             PG_UNROLL

@@ -773,8 +773,11 @@ void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
         // the packets deferred above (ANY protocol: rare): testConnection with the iphash end
         // points and the ANY-protocol first match, inline (conn_any_1), counted into the same
         // histogram; the lane replays its own tuple sequence reading only the protocol stream
+#if defined(PG_PROBE_NOPOST)  // measurement build only: the deferred pass compiled out
+        saw_any = false;
+#endif
         if (saw_any) {
-            auto one = [&](uint64_t i) { out[i] = conn_any_1<COUNT>(T, src[i], dst[i], h); };
+            auto one =[&](uint64_t i) { out[i] = conn_any_1<COUNT>(T, src[i], dst[i], h); };
             for (uint64_t qq = first; qq < nfull; qq += stride) {
                 const Words<P / 4> pw = ld_words<P / 4>(reinterpret_cast<const uint32_t*>(proto + qq * P));
                 for (int j = 0; j < P; j++)
@@ -1128,7 +1131,7 @@ static void launch_classify(const DevTableSet& T, const Tuning& tu, int t, const
         // (+ 32: the set has no PAIR tables, k_classify NOPAIR)
         const bool nopair = T.node.n_pair == 0 && PG_NODE_NOPAIR;
         // (+ 64: the uniform cross layout, k_classify UNIF)
-        const bool unif = nopair && T.node.uniform;
+        const bool unif = T.node.uniform != 0;  // (no PAIR tables either; its tries take the aligned encoding)
         auto go1 = [&](auto stage, const DevTableSet& Ts, uint32_t words) {
             constexpr int S = decltype(stage)::value;
             if constexpr (COUNT) {

@@ -43,12 +43,16 @@ struct DevTable {          // 32 B: two 16-B loads
 // Node classifier (fastpath.cpp build_node; PERPOD / CONN modes): every table the node
 // covers evaluated through one IPv4 trie and one L4-key trie shared by all tables, and one
 // cross-table entry per evaluation.
-//   img    u32[]  (tries: non-leaf entries in the node encoding, blobwalk.hpp node_entry)
-//                 IPv4 trie (root at word 0, leaf -> the node IP class's self word) | L4-key
-//                 trie (leaf -> the node key class's self word) | ipself u32[n_ipc] | kself
-//                 u32[gk] (self words: A << 10 at byte A, so a finished lookup re-reads itself
-//                 and every lookup has the trie's depth) | ipinfo uint2[n_ipc] {interface,
-//                 tin | tout << 16} | tabinfo
+//   img    u32[]  (tries: entries are byte addresses in the image, blobwalk.hpp node_child_byte)
+//                 IPv4 trie (root at word 0, leaf -> the node IP class's record) | L4-key
+//                 trie (leaf -> the node key class's record) | IPv4 class records: in the
+//                 uniform layout 16 B {self, packed end point (classify.hpp node_end_packed),
+//                 common-row mask lo, hi} from word ipinfo, else 4-B self words from word
+//                 ipself | key class records (uniform: 32 B, else 4 B) from byte kself << shift
+//                 (self = the leaf value pointing at the record: a lookup that reached a leaf
+//                 above the trie's last level re-reads it, so every lookup has the trie's depth)
+//                 | outside the uniform layout: ipinfo uint2[n_ipc] {interface, tin | tout << 16}
+//                 | tabinfo
 //                 uint4[T] {cross base, nkc | covered << 31, common row, 0} | kmap u16[T][2^gk_shift]
 //                 (local key class) | the words up to img_words_base are the base image;
 //                 then the common-row section (cmap != 0): per covered table its most
@@ -73,11 +77,11 @@ struct DevNode {
     uint32_t img_words_base;  // image without the common-row section and the dst records
     uint32_t cmap;         // word offset of the common-row bitmap in img, 0 = none
     uint32_t ip_s1, key_root, key_k1;
-    // fixed-depth tries (blobwalk.hpp node_child_byte): a leaf points at its class's self word
-    // (IPv4: ipself + class, key: kself + class, word offsets in img); every lookup takes
-    // exactly ip_depth / key_depth reads
+    // fixed-depth tries (blobwalk.hpp node_child_byte): a leaf is its class record's byte
+    // address r; class = (r >> record shift) - ipself / kself (blobwalk.hpp node_ip_rec_shift); every lookup
+    // takes exactly ip_depth / key_depth reads
     uint32_t ip_depth, key_depth, ipself, kself;
-    uint32_t ipinfo, tabinfo, kmap;  // word offsets in img
+    uint32_t ipinfo, tabinfo, kmap;  // word offsets in img (uniform: ipinfo = the IPv4 class records)
     uint32_t gk;           // node key classes
     // row strides as shifts (rows padded to powers of two, so a row address is one shifted add):
     // kmap: table t's u16 row at halfword (kmap * 2) + (t << gk_shift); common-row bitmap:
@@ -93,8 +97,9 @@ struct DevNode {
     // uniform layout (every table covered, none in PAIR form, at most 64 tables;
     // Tuning::node_uniform): table t's cross rows are over the node key classes, entry (t, ip
     // class g, key class k) at word (t * n_ipc + g) * gk + k, and its common row (when cmap != 0)
-    // at image word crow0 + t * gk; tabinfo and kmap are not read, and the common-row marks at
-    // cmap are one uint2 mask per IP class (bit t: that class's row of table t is the common one)
+    // at image word crow0 + t * gk; tabinfo and kmap are not read, and the common-row marks are
+    // one uint2 mask per IP class in its record (bit t: that class's row of table t is the
+    // common one; class g's at word cmap + (g << cmap_shift))
     uint32_t uniform, crow0;
 };
 

@@ -75,12 +75,14 @@ constexpr uint32_t kTrieFail = 0xFFFFFFFFu;
 // HBM-resident blobs: the root alone is staged in LDS, its stride capped by Tuning::lc_root_bits
 // (default 12: 16 KiB per workgroup; A/B on MI355X, config 4: 163 Gpps at 12 vs 131 at 14 --
 // the 64 KiB root of 14 bits held the launch to half the resident waves)
-// enc: kEncBlob (blobwalk.hpp trie_child / trie_stride); kEncNode, the node image's encoding
-// (blobwalk.hpp node_child_byte): a non-leaf entry holds the child's BYTE offset << 5 | stride,
-// the levels below the root take uniform strides (the bit offset of a level is a per-level
-// constant), so a step is one bit-field extract and one shifted add; kEncWords, the FD blobs' (blobwalk.hpp fd_walk): the same with
-// the child's WORD offset, children below 16 MiB.
-enum TrieEnc { kEncBlob = 0, kEncNode = 1, kEncWords = 2 };
+// enc: kEncBlob (blobwalk.hpp trie_child / trie_stride); kEncNode / kEncNodeA, the node
+// image's shifted / aligned encodings (blobwalk.hpp node_child_byte): a non-leaf entry is the
+// child's BYTE address << 5 | stride, or (aligned) the BYTE address itself with the child
+// placed at an address = its stride mod 32 (strides 8 or 4); the levels below the root take
+// uniform strides (the bit offset of a level is a per-level constant), so a step is one
+// bit-field extract and one shifted add; kEncWords, the FD blobs' (blobwalk.hpp fd_walk): the
+// child's WORD offset << 10 | stride << 5 | shift, children below 16 MiB.
+enum TrieEnc { kEncBlob = 0, kEncNode = 1, kEncWords = 2, kEncNodeA = 3 };
 constexpr uint32_t kWordsChildMax = 1u << 22;
 // cstride: the stride of the levels below the root without level compression (8; FD blobs
 // that must fit LDS try 6 and 4: more, smaller levels)
@@ -122,11 +124,16 @@ uint32_t build_trie(std::vector<uint32_t>& blob, const std::vector<uint64_t>& bn
                 else if (tu.lc_max_stride >= 16 && j.shift >= 16 && inside >= 2048) st = 16;
                 else if (inside >= tu.lc_dense12) st = 12;
             }
+            if (enc == kEncNodeA) {  // the child at a byte address = its stride mod 32 (blobwalk.hpp)
+                if (st % 4u) return kTrieFail;
+                while ((blob.size() * 4u) % 32u != st % 32u) blob.push_back(0);
+            }
             uint32_t child = (uint32_t)blob.size();
-            const uint64_t lim = enc == kEncNode ? kNodeChildMaxWords : (enc == kEncWords ? kWordsChildMax : kTrieChildMask);
+            const bool node = enc == kEncNode || enc == kEncNodeA;
+            const uint64_t lim = node ? kNodeChildMaxWords : (enc == kEncWords ? kWordsChildMax : kTrieChildMask);
             if ((uint64_t)child + (1ull << st) > lim) return kTrieFail;
             blob.resize(blob.size() + (1u << st), 0);
-            blob[j.block + e] = enc == kEncNode    ? node_entry(child, st)
+            blob[j.block + e] = node               ? node_entry(child, st, enc == kEncNodeA)
                                 : enc == kEncWords ? (child << 10 | st << 5 | (j.shift - st))
                                                    : child | (st << kTrieStrideShift);
             stack.push_back({child, a, j.shift - st, st});
@@ -682,10 +689,11 @@ bool build_fast_table(const DevRule* rules, uint32_t n, uint32_t rule_base, uint
     return true;
 }
 
-// ---- node tries: depth and fixed-depth leaves (kEncNode: child BYTE offset << 5) --------------
+// ---- node tries: depth and fixed-depth leaves (kEncNode / kEncNodeA) -------------------------
 namespace {
-uint32_t node_trie_depth(const std::vector<uint32_t>& b, uint32_t root, uint32_t s1) {
-    uint32_t d = 1;
+// visits every leaf (kLeaf | class) of a node trie with its level (root = 1)
+template <class F>
+void node_trie_leaves(const std::vector<uint32_t>& b, uint32_t root, uint32_t s1, bool aligned, F&& f) {
     struct J {
         uint32_t at, n, depth;
     };
@@ -693,27 +701,25 @@ uint32_t node_trie_depth(const std::vector<uint32_t>& b, uint32_t root, uint32_t
     while (!st.empty()) {
         J j = st.back();
         st.pop_back();
-        d = std::max(d, j.depth);
         for (uint32_t e = 0; e < j.n; e++) {
             const uint32_t v = b[j.at + e];
-            if (v & kLeaf) continue;
-            st.push_back({(v >> 5) / 4u, 1u << (v & 31u), j.depth + 1});
+            if (v & kLeaf) f(j.at + e, v & ~kLeaf, j.depth);
+            else st.push_back({(aligned ? v : v >> 5) / 4u, 1u << (v & 31u), j.depth + 1});
         }
     }
+}
+uint32_t node_trie_depth(const std::vector<uint32_t>& b, uint32_t root, uint32_t s1, bool aligned) {
+    uint32_t d = 1;
+    node_trie_leaves(b, root, s1, aligned, [&](uint32_t, uint32_t, uint32_t depth) { d = std::max(d, depth); });
     return d;
 }
-// leaves (kLeaf | class) -> pointers to self words (class c: word self0 + c)
-void node_point_leaves(std::vector<uint32_t>& b, uint32_t root, uint32_t s1, uint32_t self0) {
-    std::vector<std::pair<uint32_t, uint32_t>> st{{root, 1u << s1}};
-    while (!st.empty()) {
-        auto j = st.back();
-        st.pop_back();
-        for (uint32_t e = 0; e < j.second; e++) {
-            uint32_t& v = b[j.first + e];
-            if (v & kLeaf) v = ((self0 + (v & ~kLeaf)) * 4u) << 5;
-            else st.push_back({(v >> 5) / 4u, 1u << (v & 31u)});
-        }
-    }
+// leaves (kLeaf | class) -> their class records (class c at rec0 + (c << shift) bytes, the
+// address itself or shifted: blobwalk.hpp node_child_byte)
+void node_point_leaves(std::vector<uint32_t>& b, uint32_t root, uint32_t s1, bool aligned, uint32_t rec0_bytes,
+                       uint32_t shift) {
+    std::vector<std::pair<uint32_t, uint32_t>> at;
+    node_trie_leaves(b, root, s1, aligned, [&](uint32_t pos, uint32_t c, uint32_t) { at.push_back({pos, c}); });
+    for (auto& p : at) b[p.first] = node_entry((rec0_bytes + (p.second << shift)) / 4u, 0u, aligned);
 }
 }  // namespace
 
@@ -861,7 +867,7 @@ void build_common_rows(HostTableSet& h, const std::vector<uint32_t>& cov, const 
     const uint64_t bits = (uint64_t)T << (rs + 5);
     if (!tu.node_common || bits > kCommonMapMaxBits) return;
     const std::vector<uint32_t>& X = h.node_cross;
-    std::vector<uint32_t> sec, map((size_t)(bits / 32), 0);
+    std::vector<uint32_t> sec, map(uni ? 0 : (size_t)(bits / 32), 0);
     // uniform layout: the marks as one 64-bit mask per IP class (uint2 {tables 0-31, 32-63}), so a
     // connection reads its two classes' masks once instead of one bitmap word per evaluation
     std::vector<uint32_t> masks(uni ? 2 * (size_t)G : 0, 0);
@@ -894,11 +900,16 @@ void build_common_rows(HostTableSet& h, const std::vector<uint32_t>& cov, const 
     const uint32_t s0 = (uint32_t)img.size();
     for (uint32_t t : cov) img[N.tabinfo + 4 * t + 2] = s0 + crow[t];
     img.insert(img.end(), sec.begin(), sec.end());
-    while (img.size() % 2) img.push_back(0);
-    N.cmap = (uint32_t)img.size();
-    N.cmap_shift = uni ? 0u : rs;
-    if (uni) img.insert(img.end(), masks.begin(), masks.end());
-    else img.insert(img.end(), map.begin(), map.end());
+    if (uni) {  // the masks live in the class records (words 2-3): class g's at word cmap + (g << 2)
+        N.cmap = N.ipinfo + 2u;
+        N.cmap_shift = 2u;
+        for (uint32_t g = 0; g < G; g++)
+            img[N.cmap + 4 * (size_t)g] = masks[2 * (size_t)g], img[N.cmap + 4 * (size_t)g + 1] = masks[2 * (size_t)g + 1];
+    } else {
+        N.cmap = (uint32_t)img.size();
+        N.cmap_shift = rs;
+        img.insert(img.end(), map.begin(), map.end());
+    }
     while (img.size() % 4) img.push_back(0);
     N.img_words = (uint32_t)img.size();
 }
@@ -967,7 +978,7 @@ bool build_node(HostTableSet& h, const std::vector<TableAnalysis*>& an, const st
         }
         gcls[k] = it->second;
     }
-    const uint32_t G = (uint32_t)ipc_key.size();
+    uint32_t G = (uint32_t)ipc_key.size();
     uint64_t entries = 0;
     for (uint32_t t : cov)
         entries += an[t]->pair ? (uint64_t)an[t]->nsc * an[t]->ndc + (uint64_t)an[t]->npc * an[t]->nkc
@@ -998,57 +1009,155 @@ bool build_node(HostTableSet& h, const std::vector<TableAnalysis*>& an, const st
         kcls[k] = it->second;
     }
     const uint32_t GK = (uint32_t)kc_key.size();
-    // uniform layout (DevNode uniform): every table covered, none in PAIR form -- rows over the
-    // node key classes at cross[(t * G + ip class) * GK + key class], so an evaluation computes
-    // its entry's address from (t, classes) instead of reading tabinfo and kmap
-    // (at most 64 tables: the common-row marks are then one 64-bit mask per IP class)
-    const bool uni = tu.node_uniform && C == T && PC == 0 && T <= 64 && (uint64_t)T * G < (1u << 24) &&
-                     (uint64_t)T * G * GK <= kNodeCrossBudget;
-    if (uni) entries = (uint64_t)T * G * GK;
-
-    // image: tries, ipinfo, tabinfo, kmap
+    // image: IPv4 trie (root at word 0), key trie, class records, tabinfo, kmap
     std::vector<uint32_t>& img = h.node_img;
     DevNode& N = h.node;
+    // end points pack into one record word (classify.hpp node_end_packed): interface indices
+    // below 2^14, fewer than 255 tables
+    bool pack_ok = T < 255;
+    for (const auto& k : ipc_key)
+        if ((int32_t)k[0] >= 0 && (k[0] & ~(3u << kEndKindShift)) >= 0x4000u) pack_ok = false;
+    // uniform layout (DevNode uniform): every table covered, none in PAIR form -- rows over the
+    // node key classes at cross[(t * G + ip class) * GK + key class], so an evaluation computes
+    // its entry's address from (t, classes) instead of reading tabinfo and kmap (at most 64
+    // tables: the common-row marks are then one 64-bit mask per IP class). Its tries take the
+    // aligned encoding (blobwalk.hpp: one VALU less per step, strides of 8 and 4 only); other
+    // node sets the shifted one, whose strides are free (config 6: a 4-KiB smaller image keeps
+    // three workgroups per CU)
+    const bool aligned = tu.node_uniform && C == T && PC == 0 && T <= 64 && pack_ok;
+    const int enc = aligned ? kEncNodeA : kEncNode;
     // IPv4 trie root: the smallest trie among the root strides that give the fewest levels (a
     // walk reads exactly depth words; a smaller image leaves LDS for the counter histogram --
-    // config 5: 12 -> 10 bits keeps image + histogram within two workgroups per CU)
+    // config 5: 12 -> 10 bits keeps image + histogram within two workgroups per CU); aligned:
+    // strides of 8 and 4 below the root, so 32 - root is a multiple of 4
     {
         const uint32_t top = std::min(pick_stride(gb.size(), 32, tu), tu.node_root_bits);
         uint32_t best_d = ~0u;
         std::vector<uint32_t> tmp;
-        for (uint32_t s1 = top; s1 + 4 > top && s1 >= 4; s1--) {
+        for (uint32_t s1 = aligned ? top - top % 4u : top; s1 >= 4 && (aligned || s1 + 4 > top); s1 -= aligned ? 4 : 1) {
             tmp.clear();
-            if (build_trie(tmp, gb, gcls, 32, s1, tu, false, kEncNode, kNodeStride) != 0) return false;
-            const uint32_t d = node_trie_depth(tmp, 0, s1);
+            if (build_trie(tmp, gb, gcls, 32, s1, tu, false, enc, kNodeStride) != 0) return false;
+            const uint32_t d = node_trie_depth(tmp, 0, s1, aligned);
             if (d < best_d || (d == best_d && tmp.size() < img.size())) {
                 best_d = d;
                 N.ip_s1 = s1;
                 img.swap(tmp);
             }
         }
+        if (best_d == ~0u) return false;
     }
-    N.key_k1 = std::min(pick_stride(kb.size(), 18, tu), tu.node_root_bits);
-    N.key_root = build_trie(img, kb, kcls, 18, N.key_k1, tu, false, kEncNode, kNodeStride);
-    if (N.key_root == kTrieFail) return false;
-    // fixed depth: leaves -> self words of their classes (DevNode)
-    N.ip_depth = node_trie_depth(img, 0, N.ip_s1);
-    N.key_depth = node_trie_depth(img, N.key_root, N.key_k1);
-    N.ipself = (uint32_t)img.size();
-    for (uint32_t g = 0; g < G; g++) img.push_back(((N.ipself + g) * 4u) << 5);
-    N.kself = (uint32_t)img.size();
-    for (uint32_t g = 0; g < GK; g++) img.push_back(((N.kself + g) * 4u) << 5);
+    N.ip_depth = node_trie_depth(img, 0, N.ip_s1, aligned);
+    // class records (blobwalk.hpp node_ip_rec_shift): uniform 16 B (IPv4) / 32 B (key), else
+    // 4-B self words
+    const uint32_t rshift = aligned ? node_ip_rec_shift<true>() : node_ip_rec_shift<false>();
+    const uint32_t kshift = aligned ? node_key_rec_shift<true>() : node_key_rec_shift<false>();
+    if (aligned) {
+        // a class with a leaf above the last level needs its record on a 32-byte boundary (a
+        // finished lookup re-reads it at stride 0), so those classes take every other record
+        // slot; the rest fill the others (slots past the classes: never reached)
+        const uint32_t align = 32u >> rshift;
+        std::vector<uint8_t> early(G, 0);
+        node_trie_leaves(img, 0, N.ip_s1, true, [&](uint32_t, uint32_t c, uint32_t d) {
+            if (d < N.ip_depth) early[c] = 1;
+        });
+        uint32_t ne = 0;
+        for (uint32_t g = 0; g < G; g++) ne += early[g];
+        const uint32_t S = std::max<uint32_t>(G, ne ? (ne - 1) * align + 1 : 0);
+        std::vector<uint32_t> slot(G);
+        std::vector<uint8_t> used(S, 0);
+        uint32_t k = 0, nx = 0;
+        for (uint32_t g = 0; g < G; g++)
+            if (early[g]) slot[g] = align * k++, used[slot[g]] = 1;
+        for (uint32_t g = 0; g < G; g++) {
+            if (early[g]) continue;
+            while (used[nx]) nx++;
+            slot[g] = nx, used[nx] = 1;
+        }
+        std::vector<std::vector<uint32_t>> rk(S, ipc_key[0]);
+        for (uint32_t g = 0; g < G; g++) rk[slot[g]] = ipc_key[g];
+        ipc_key.swap(rk);
+        std::vector<std::pair<uint32_t, uint32_t>> lv;
+        node_trie_leaves(img, 0, N.ip_s1, true, [&](uint32_t pos, uint32_t c, uint32_t) { lv.push_back({pos, c}); });
+        for (auto& x : lv) img[x.first] = kLeaf | slot[x.second];
+        G = S;
+    }
+    entries = 0;
+    for (uint32_t t : cov)
+        entries += an[t]->pair ? (uint64_t)an[t]->nsc * an[t]->ndc + (uint64_t)an[t]->npc * an[t]->nkc
+                               : (uint64_t)G * an[t]->nkc;
+    if (entries > kNodeCrossBudget) return false;
+    const bool uni = aligned && (uint64_t)T * G < (1u << 24) && (uint64_t)T * G * GK <= kNodeCrossBudget;
+    if (aligned && !uni) {  // (the aligned tries are the uniform layout's): the other layout
+        Tuning t2 = tu;
+        t2.node_uniform = 0;
+        return build_node(h, an, pods, node_end, t2);
+    }
+    if (uni) entries = (uint64_t)T * G * GK;
+    // L4-key trie: aligned, the root stride (18 - root a multiple of 4, at most 8 bits: a 10-bit
+    // root saves a level but its 4 KiB cost config 3 a workgroup per CU) with the fewest levels,
+    // then the smallest trie
+    if (aligned) {
+        const size_t k0 = img.size();
+        std::vector<uint32_t> best;
+        uint32_t best_d = ~0u;
+        for (uint32_t k1 = 2; k1 <= std::min(tu.node_root_bits, 8u); k1 += 4) {
+            img.resize(k0);
+            const uint32_t root = build_trie(img, kb, kcls, 18, k1, tu, false, enc, kNodeStride);
+            if (root == kTrieFail) continue;
+            const uint32_t d = node_trie_depth(img, root, k1, true);
+            if (d < best_d || (d == best_d && img.size() < k0 + best.size())) {
+                best_d = d;
+                N.key_k1 = k1;
+                N.key_root = root;
+                best.assign(img.begin() + k0, img.end());
+            }
+        }
+        if (best_d == ~0u) return false;
+        img.resize(k0);
+        img.insert(img.end(), best.begin(), best.end());
+    } else {
+        N.key_k1 = std::min(pick_stride(kb.size(), 18, tu), tu.node_root_bits);
+        N.key_root = build_trie(img, kb, kcls, 18, N.key_k1, tu, false, enc, kNodeStride);
+        if (N.key_root == kTrieFail) return false;
+    }
+    N.key_depth = node_trie_depth(img, N.key_root, N.key_k1, aligned);
+    // records: uniform IPv4 classes {self, packed end point, common-row mask lo, hi} (16 B), key
+    // classes {self} (32 B); otherwise 4-B self words and ipinfo {interface, tin | tout << 16}
+    // per class; self = the leaf value pointing at the record (blobwalk.hpp)
+    const uint32_t rw = (1u << rshift) / 4u, kw = (1u << kshift) / 4u;  // record words
+    while (img.size() % 8) img.push_back(0);
+    const uint32_t irec0 = (uint32_t)img.size();
+    img.resize(img.size() + rw * (size_t)G, 0);
+    while (img.size() % 8) img.push_back(0);
+    const uint32_t krec0 = (uint32_t)img.size();
+    img.resize(img.size() + kw * (size_t)GK, 0);
     if ((uint64_t)img.size() * 4 >= kNodeChildMaxWords * 4ull) return false;
-    node_point_leaves(img, 0, N.ip_s1, N.ipself);
-    node_point_leaves(img, N.key_root, N.key_k1, N.kself);
-    while (img.size() % 2) img.push_back(0);
-    N.ipinfo = (uint32_t)img.size();
+    node_point_leaves(img, 0, N.ip_s1, aligned, irec0 * 4u, rshift);
+    node_point_leaves(img, N.key_root, N.key_k1, aligned, krec0 * 4u, kshift);
     for (uint32_t g = 0; g < G; g++) {
         const auto& k = ipc_key[g];
-        auto t16 = [](uint32_t t) { return (int32_t)t < 0 ? 0xFFFFu : t; };
-        img.push_back(k[0]);
-        img.push_back(t16(k[1]) | (t16(k[2]) << 16));
+        uint32_t* r = img.data() + irec0 + rw * (size_t)g;
+        r[0] = node_entry(irec0 + rw * g, 0u, aligned);
+        if (aligned) {
+            auto t8 = [](uint32_t t) { return (int32_t)t < 0 ? 0xFFu : t; };
+            const uint32_t f = (int32_t)k[0] < 0 ? 0xFFFFu : ((k[0] & 0x3FFFu) | ((k[0] >> kEndKindShift) & 3u) << 14);
+            r[1] = f | t8(k[1]) << 16 | t8(k[2]) << 24;
+        }
     }
-    while (img.size() % 4) img.push_back(0);
+    for (uint32_t k = 0; k < GK; k++) img[krec0 + kw * k] = node_entry(krec0 + kw * k, 0u, aligned);
+    N.ipself = irec0 * 4u >> rshift;  // class = (record byte address >> record shift) - ipself
+    N.kself = krec0 * 4u >> kshift;
+    N.ipinfo = irec0;
+    if (!aligned) {
+        while (img.size() % 2) img.push_back(0);
+        N.ipinfo = (uint32_t)img.size();
+        auto t16 = [](uint32_t t) { return (int32_t)t < 0 ? 0xFFFFu : t; };
+        for (uint32_t g = 0; g < G; g++) {
+            img.push_back(ipc_key[g][0]);
+            img.push_back(t16(ipc_key[g][1]) | (t16(ipc_key[g][2]) << 16));
+        }
+        while (img.size() % 4) img.push_back(0);
+    }
     N.tabinfo = (uint32_t)img.size();
     img.resize(img.size() + 4 * (size_t)T, 0);
     N.gk_shift = 0;
