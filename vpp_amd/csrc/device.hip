@@ -452,14 +452,37 @@ constexpr size_t kLdsPerCU = 160u << 10;
 #define PG_NODE_FULLH 1
 #endif
 // CONN over a uniform node (STAGE + 96): ANY-protocol packets, the only ones the node cannot
-// classify, are deferred to a pass after the main loop (the per-table path, counted into the
-// same histogram), so the loop carries no per-table fallback. The out-of-line fallback call
-// in the loop cost the whole kernel its SGPR allocation: 54 SGPRs spilled to VGPR lanes, a
-// v_readlane per use (A/B on MI355X, a build without the fallback: config 5 with counters
-// 123 -> 139 Gpps, without 152 -> 167.5; PERPOD unchanged, so it keeps the call)
+// classify, are deferred to k_conn_any, launched after the classify kernel on the same stream
+// (iphash end points, the ANY-protocol first match, global counter increments), so the
+// classify kernel carries no per-table fallback. The out-of-line fallback call in the loop
+// cost the kernel its SGPR allocation: 54 SGPRs spilled to VGPR lanes, a v_readlane per use;
+// a pass after the loop in the same kernel still cost 6 % (A/B on MI355X, config 5 with
+// counters: in-loop call 123, pass after the loop 129, no pass 137 Gpps; PERPOD unchanged by
+// any of it, so it keeps the call). A launch that deferred a packet marks its slot of a ring
+// with its sequence number; the k_conn_any launch of the same number classifies the batch's
+// ANY-protocol packets when it finds it, and returns at once otherwise.
 #ifndef PG_CONN_DEFER_ANY
 #define PG_CONN_DEFER_ANY 1
 #endif
+constexpr uint32_t kAnySlots = 4096;  // (a power of two)
+__device__ uint32_t g_any_seq[kAnySlots];
+// any of the four protocol bytes of w above 2 (bytes >= 0x80 by their top bit, the rest by a
+// carry-free add into it)
+__device__ __forceinline__ bool any_proto_gt2(uint32_t w) {
+    return ((((w & 0x7F7F7F7Fu) + 0x7D7D7D7Du) | w) & 0x80808080u) != 0u;
+}
+
+template <bool COUNT>
+__global__ __launch_bounds__(kBlock) void k_conn_any(DevTableSet T, const uint32_t* __restrict__ src,
+                                                  const uint32_t* __restrict__ dst, const uint8_t* __restrict__ proto,
+                                                  uint64_t n, uint32_t* __restrict__ out, unsigned long long* counters,
+                                                  uint32_t seq) {
+    if (g_any_seq[seq & (kAnySlots - 1u)] != seq) return;
+    const Hist h{nullptr, counters};  // global increments (rare packets)
+    const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride)
+        if (proto[i] > 2u) out[i] = conn_any_1<COUNT>(T, src[i], dst[i], h);
+}
 #ifndef PG_TPL  // tuples per lane per loop iteration (4 or 8)
 #define PG_TPL 4
 #endif
@@ -546,7 +569,7 @@ void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
                                                      const uint16_t* __restrict__ dport,
                                                      const uint8_t* __restrict__ proto, uint64_t n,
                                                      uint32_t* __restrict__ out, unsigned long long* counters,
-                                                     uint32_t stage_words, uint32_t hist_cells) {
+                                                     uint32_t stage_words, uint32_t hist_cells, uint32_t any_seq) {
     constexpr int STAGE = STAGE_ & 7;
     constexpr bool NODST = MODE == 0 && (STAGE_ & 8);
     // STAGE_ + 16 (node kernels with counters): the LDS histogram holds every slot (launcher)
@@ -558,7 +581,6 @@ void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
     constexpr bool UNIF = NODE && NOPAIR && (STAGE_ & 64);
     // CONN over a uniform node: ANY-protocol packets deferred past the main loop (PG_CONN_DEFER_ANY)
     constexpr bool DEFER = UNIF && MODE == 2 && PG_CONN_DEFER_ANY;
-    bool saw_any = false;  // (DEFER) this lane deferred a packet
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     uint32_t* hist = smem + (STAGE ? stage_words : 0u);
     // node kernels: the LDS histogram, when used, holds every slot (HistT<true>: no window test)
@@ -685,6 +707,14 @@ void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
     // once after the first chunk's cross-entry loads are issued (node kernels, PF 2)
     auto run_group = [&](const Group& g, uint64_t qq, auto&& hk) {
         uint32_t sv[P], dv[P], spv[P], dpv[P], prv[P], o[P];
+        // (DEFER) a protocol code > 2 among the group's: mark this launch's ring slot for
+        // k_conn_any (one test of the packed protocol word per group, no state across groups)
+        if constexpr (DEFER) {
+            bool any = false;
+#pragma unroll
+            for (int k = 0; k < P / 4; k++) any |= any_proto_gt2(g.pr.w[k]);
+            if (any) g_any_seq[any_seq & (kAnySlots - 1u)] = any_seq;
+        }
 #pragma unroll
         for (int j = 0; j < P; j++) {
             sv[j] = g.s.w[j];
@@ -692,7 +722,6 @@ void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
             dpv[j] = (g.dp.w[j / 2] >> (16 * (j & 1))) & 0xFFFFu;
             spv[j] = (g.sp.w[j / 2] >> (16 * (j & 1))) & 0xFFFFu;
             prv[j] = (g.pr.w[j / 4] >> (8 * (j & 3))) & 0xFFu;
-            if (DEFER) saw_any |= prv[j] > 2u;
         }
 #if PG_PROBE_STREAM
         for (int j = 0; j < P; j++) o[j] = sv[j] ^ dv[j] ^ dpv[j] ^ prv[j] ^ spv[j];
@@ -767,26 +796,10 @@ void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
         else if constexpr (NODE) classify_node_q<MODE, COUNT, 1, STAGE && PG_PRED, STAGE == 3, NOPAIR, UNIF, DEFER>(T, T.node, img, s1, d1, sp1, dp1, pr1, h, o);
         else classify_q<MODE, COUNT, 1, STAGE == 1 && PG_PRED>(T, blobs, tab0, s1, d1, sp1, dp1, pr1, h, o, rootb);
         out[i] = o[0];
-        if (DEFER) saw_any |= pr1[0] > 2u;
+        if (DEFER && pr1[0] > 2u) g_any_seq[any_seq & (kAnySlots - 1u)] = any_seq;
     }
-    if constexpr (DEFER) {
-        // the packets deferred above (ANY protocol: rare): testConnection with the iphash end
-        // points and the ANY-protocol first match, inline (conn_any_1), counted into the same
-        // histogram; the lane replays its own tuple sequence reading only the protocol stream
-#if defined(PG_PROBE_NOPOST)  // measurement build only: the deferred pass compiled out
-        saw_any = false;
-#endif
-        if (saw_any) {
-            auto one =[&](uint64_t i) { out[i] = conn_any_1<COUNT>(T, src[i], dst[i], h); };
-            for (uint64_t qq = first; qq < nfull; qq += stride) {
-                const Words<P / 4> pw = ld_words<P / 4>(reinterpret_cast<const uint32_t*>(proto + qq * P));
-                for (int j = 0; j < P; j++)
-                    if (((pw.w[j / 4] >> (8 * (j & 3))) & 0xFFu) > 2u) one(qq * P + j);
-            }
-            for (uint64_t i = nfull * P + first; i < n; i += stride)
-                if (proto[i] > 2u) one(i);
-        }
-    }
+    // (the packets deferred above -- ANY protocol, rare -- are classified by k_conn_any, launched
+    // after this kernel on the same stream)
     if (COUNT) {
         h.flush_hot();
         __syncthreads();
@@ -1014,8 +1027,20 @@ static void launch_bs(const DevTableSet& T, const Tuning& tu, int t, const uint3
     // three times; with counters no difference): fewer streams in flight per CU contend less
     const uint32_t bpc = tu.blocks_per_cu ? tu.blocks_per_cu : (MODE == 0 && (STAGE & 7) == 4 && !COUNT ? 2u : 0u);
     const size_t lds = hist + (size_t)stage * 4;
+    // CONN over a uniform node: the launch's number for its deferred ANY-protocol packets, and
+    // k_conn_any after it (PG_CONN_DEFER_ANY)
+    constexpr bool defer = MODE == 2 && NODE && (STAGE & 32) && (STAGE & 64) && PG_CONN_DEFER_ANY;
+    static std::atomic<uint32_t> launch_seq{1};
+    uint32_t seq = 0;
+    if constexpr (defer) {
+        seq = launch_seq.fetch_add(1, std::memory_order_relaxed);
+        if (seq == 0) seq = launch_seq.fetch_add(1, std::memory_order_relaxed);  // (0: never written)
+    }
     hipLaunchKernelGGL(k, dim3(grid_resident(k, BS, lds, items, bpc)), dim3(BS), lds, st, T, t, src, dst, sport, dport,
-                       proto, n, out, counters, stage, cells);
+                       proto, n, out, counters, stage, cells, seq);
+    if constexpr (defer)
+        hipLaunchKernelGGL(k_conn_any<COUNT>, dim3(grid_for(n)), dim3(kBlock), 0, st, T, src, dst, proto, n, out,
+                           counters, seq);
 }
 
 // Workgroup size: a staged image is shared by the workgroup, so larger workgroups hold more
