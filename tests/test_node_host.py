@@ -267,6 +267,42 @@ def test_config6_pair_table_covered():
     assert np.array_equal(got >> 30, act.astype(np.uint32)) and np.array_equal(got & 0x3FFFFFFF, slot)
 
 
+def test_uniform_records_with_mostly_range_classes():
+    """Aligned node tries (uniform layout): a class with a leaf above the trie's last level
+    needs a 32-byte aligned record, so such classes take every other record slot. With few
+    pods and many source ranges most classes are ranges, the slots outnumber the classes
+    (unused slots between them), and the node still equals the per-table path and the oracle."""
+    rnd = random.Random(91)
+    e = R.Engine(0)
+    e.SetMainInterfaceName("GbE")
+    e.SetVxlanBVIIfName("VXLAN-BVI")
+    e.SetHostInterconnectIfName("VPP-Host")
+    local, pod_ips, ops = {}, [], []
+    for k in range(3):
+        ip = 0x0A0A0000 | (k + 1)
+        pod_ips.append(ip)
+        e.SetPodIfName("ns/p%d" % k, "tap%d" % k)
+        e.RegisterPod("ns/p%d" % k, W.ip_str(ip), False)
+        local[ip] = "tap%d" % k
+    ranges = [{"action": rnd.choice([0, 1, 2]), "src": "%d.%d.%d.0/%d" % (10 + k % 3, k, (7 * k) % 256, rnd.choice([20, 22, 24])),
+               "dst": ""} for k in range(120)]
+    for k in range(3):
+        ops.append(("config/vpp/acls/v2/acl/out-tap%d" % k, {"name": "out-tap%d" % k, "rules": ranges[40 * k:40 * k + 40]
+                                                              + [{"action": 0, "src": "", "dst": ""}],
+                                                              "ingress": [], "egress": ["tap%d" % k]}))
+    ops.append(("config/vpp/acls/v2/acl/g", {"name": "g", "rules": ranges[::2] + [{"action": 1, "src": "", "dst": ""}],
+                                             "ingress": [], "egress": ["VXLAN-BVI"]}))
+    e.ApplyTxn(True, ops)
+    ns = e.node_stats()
+    assert ns["uniform"], ns
+    anchors = [int(np.uint32((10 + k % 3) << 24 | k << 16 | ((7 * k) % 256) << 8)) for k in range(120)]
+    rng = np.random.default_rng(92)
+    src, dst, sport, dport, proto = fz.rand_tuples(rng, 30000, anchors + pod_ips, any_pct=0.02)
+    m = rng.random(len(src)) < 0.5
+    dst[m] = np.array(pod_ips, np.uint32)[rng.integers(0, len(pod_ips), int(m.sum()))]
+    check(e, (local, []), (src, dst, sport, dport, proto))
+
+
 @pytest.mark.parametrize("config", [3, 5])
 def test_uniform_cross_layout_equals_per_table_layout(config):
     """The node's uniform cross layout (rows over the node key classes, addresses computed) and

@@ -486,6 +486,11 @@ __global__ __launch_bounds__(kBlock) void k_conn_any(DevTableSet T, const uint32
 #ifndef PG_TPL  // tuples per lane per loop iteration (4 or 8)
 #define PG_TPL 4
 #endif
+#ifndef PG_TPL_CONN  // ... in CONN mode: 8 (A/B on MI355X, config 5 with counters 133.7 -> 137.7 Gpps,
+#define PG_TPL_CONN 8  // without 163.3 -> 165.7; PERPOD and SINGLE lose at 8: config 3 334 -> 238)
+#endif
+template <int MODE>
+constexpr int tuples_per_lane() { return MODE == 2 ? PG_TPL_CONN : PG_TPL; }
 
 // NW consecutive u32 of a stream with the widest loads / stores (NW = 1, 2, 4, 8)
 template <int NW>
@@ -660,10 +665,10 @@ void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
     if (STAGE || COUNT) __syncthreads();
     const uint64_t stride = (uint64_t)gridDim.x * BS;
     const uint64_t first = (uint64_t)blockIdx.x * BS + threadIdx.x;
-    // full groups of P tuples per lane (P = PG_TPL): SoA fields read with 16/8/4-byte loads per
+    // full groups of P tuples per lane (P = tuples_per_lane): SoA fields read with 16/8/4-byte loads per
     // lane (coalesced, non-temporal); prefetch 1/2: the next group's loads are in flight
     // while this group is classified
-    constexpr int P = PG_TPL;
+    constexpr int P = tuples_per_lane<MODE>();
     const uint64_t nfull = VEC ? (n / P) : 0;
     struct Group {
         Words<P> s, d;
@@ -1123,7 +1128,7 @@ static void launch_classify(const DevTableSet& T, const Tuning& tu, int t, const
             hist = ((size_t)cells + 1u) * 8;
         }
     }
-    const uint64_t items = VEC ? (n + PG_TPL - 1) / PG_TPL : n;
+    const uint64_t items = VEC ? (n + tuples_per_lane<MODE>() - 1) / tuples_per_lane<MODE>() : n;
     if constexpr (MODE == 0) {
         const DevTable& hd = T.host_tabs[t];
         const uint32_t words = T.host_blob_words[t];
@@ -1210,7 +1215,8 @@ int dev_classify(const DevTableSet& T, const Tuning& tu, int mode, int table_id,
     if (n == 0) return 0;
     auto al = [](const void* p, uintptr_t a) { return ((uintptr_t)p & (a - 1)) == 0; };
     // the group loads: 4*P-byte src/dst/out (16-B pieces), 2*P-byte ports, P-byte protocols
-    constexpr uintptr_t kPort = 2 * PG_TPL > 16 ? 16 : 2 * PG_TPL, kProto = PG_TPL > 16 ? 16 : PG_TPL;
+    const uintptr_t P = mode == 2 ? tuples_per_lane<2>() : tuples_per_lane<0>();
+    const uintptr_t kPort = 2 * P > 16 ? 16 : 2 * P, kProto = P > 16 ? 16 : P;
     const bool vec = al(src, 16) && al(dst, 16) && al(dport, kPort) && al(proto, kProto) && al(out, 16) &&
                      (mode != 2 || al(sport, kPort));
     hipStream_t st = (hipStream_t)stream;

@@ -1079,6 +1079,8 @@ bool build_node(HostTableSet& h, const std::vector<TableAnalysis*>& an, const st
         std::vector<std::pair<uint32_t, uint32_t>> lv;
         node_trie_leaves(img, 0, N.ip_s1, true, [&](uint32_t pos, uint32_t c, uint32_t) { lv.push_back({pos, c}); });
         for (auto& x : lv) img[x.first] = kLeaf | slot[x.second];
+        if (std::getenv("PG_NODE_DEBUG"))  // measurement aid: record slots
+            std::fprintf(stderr, "node: %u classes, %u with a leaf above the last level, %u record slots\n", G, ne, S);
         G = S;
     }
     entries = 0;
