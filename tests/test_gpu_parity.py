@@ -338,6 +338,38 @@ def test_conn_any_protocol_packets_deferred(any_pct):
     assert np.array_equal(c, hist), np.nonzero(c != hist)[0][:10]
 
 
+def test_conn_any_protocol_concurrent_streams():
+    """k_conn_any finds its own launch's mark: CONN launches on two streams in flight together,
+    one batch with ANY-protocol packets and one without, then the other way round; every
+    verdict equals the oracle's."""
+    from oracle.world import World
+    from vpp_amd import workloads as W
+    w = W.config5(0, n_tuples=(1 << 17) + 3)
+    e = w.engine
+    wd = World(e, w.local_ifs, w.node_if)
+    b0 = D.TupleBatch(w.n_tuples, with_sport=True)
+    D.gen_tuples(e, b0, **w.gen)
+    src, dst, sport, dport, proto = b0.numpy(b0.n)
+    rng = np.random.default_rng(12)
+    proto_any = proto.copy()
+    m = rng.random(b0.n) < 0.03
+    proto_any[m] = 7
+    batches = [D.TupleBatch.from_numpy(src, dst, sport, dport, proto_any), D.TupleBatch.from_numpy(src, dst, sport, dport, proto)]
+    expect = [wd.conn(src, dst, sport, dport, p, threads=16)[0] for p in (proto_any, proto)]
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    for order in ((0, 1), (1, 0)):
+        outs = [torch.empty(b0.n, dtype=torch.int32, device="cuda") for _ in range(2)]
+        torch.cuda.synchronize()
+        for k in order:
+            with torch.cuda.stream(streams[k]):
+                for _ in range(3):  # several launches per stream: several ring slots in flight
+                    D.classify(e, MODE_CONN, -1, batches[k], outs[k])
+        torch.cuda.synchronize()
+        for k in range(2):
+            got = outs[k].cpu().numpy().view(np.uint32)
+            assert ((got >> 30) == expect[k].astype(np.uint32)).all(), (order, k)
+
+
 @pytest.mark.parametrize("mode", [MODE_PERPOD, MODE_CONN])
 def test_k8s_object_cluster_gpu_vs_oracle(mode):
     """The cluster given as K8s objects (policy cache -> processor -> configurator -> renderer,
