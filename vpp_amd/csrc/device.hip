@@ -466,6 +466,9 @@ constexpr size_t kLdsPerCU = 160u << 10;
 #endif
 constexpr uint32_t kAnySlots = 4096;  // (a power of two)
 __device__ uint32_t g_any_seq[kAnySlots];
+// launch numbers, one sequence for the process (every launch_bs instantiation draws from it:
+// concurrent launches must not share a ring slot with different numbers)
+static std::atomic<uint32_t> g_launch_seq{1};
 // any of the four protocol bytes of w above 2 (bytes >= 0x80 by their top bit, the rest by a
 // carry-free add into it)
 __device__ __forceinline__ bool any_proto_gt2(uint32_t w) {
@@ -1035,11 +1038,10 @@ static void launch_bs(const DevTableSet& T, const Tuning& tu, int t, const uint3
     // CONN over a uniform node: the launch's number for its deferred ANY-protocol packets, and
     // k_conn_any after it (PG_CONN_DEFER_ANY)
     constexpr bool defer = MODE == 2 && NODE && (STAGE & 32) && (STAGE & 64) && PG_CONN_DEFER_ANY;
-    static std::atomic<uint32_t> launch_seq{1};
     uint32_t seq = 0;
     if constexpr (defer) {
-        seq = launch_seq.fetch_add(1, std::memory_order_relaxed);
-        if (seq == 0) seq = launch_seq.fetch_add(1, std::memory_order_relaxed);  // (0: never written)
+        seq = g_launch_seq.fetch_add(1, std::memory_order_relaxed);
+        if (seq == 0) seq = g_launch_seq.fetch_add(1, std::memory_order_relaxed);  // (0: never written)
     }
     hipLaunchKernelGGL(k, dim3(grid_resident(k, BS, lds, items, bpc)), dim3(BS), lds, st, T, t, src, dst, sport, dport,
                        proto, n, out, counters, stage, cells, seq);
