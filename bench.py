@@ -52,7 +52,11 @@ def parse():
     p.add_argument("--counters", action="store_true", help="time with per-rule hit counters on")
     p.add_argument("--cpu-sample", type=int, default=16 << 20, help="tuples in the CPU-baseline sample")
     p.add_argument("--faithful-seconds", type=float, default=8.0,
-                   help="budget of the single-thread reference-faithful CPU variant (SINGLE mode)")
+                   help="budget of the single-thread reference-faithful CPU variant")
+    p.add_argument("--side", default="auto",
+                   help="configs timed after the main line in labelled side blocks, same launches and "
+                        "self-check (comma list, 'none'; auto = 3 when the main config is 2 without "
+                        "--rules / --counters: the 10k-rule per-pod config north_star names)")
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--check-tuples", type=int, default=1 << 20,
                    help="tuples of every rank's shard checked against the oracle after the timed region")
@@ -211,10 +215,69 @@ def main():
         line["parity_per_rank"] = pars
     if rank == 0 and world == 1 and not a.no_cpu:
         line["cpu_baseline"] = cpu_baseline(w, b, out, a.cpu_sample, a.faithful_seconds, a.cpu_seconds)
+    side = a.side if a.side != "auto" else ("3" if a.config == 2 and not a.rules and not a.counters and
+                                             not a.tuples and not a.per_table else "none")
+    if side != "none":
+        del b, out, counters
+        torch.cuda.empty_cache()
+        for c in side.split(","):
+            line["side_config%s" % c] = side_line(a, int(c), rank, world, local, launched, check_threads)
     if rank == 0:
         print(json.dumps(line), file=json_out, flush=True)
     if launched:
         dist.destroy_process_group()
+
+
+def side_line(a, config, rank, world, local, launched, check_threads):
+    """A labelled side block of the bench line: config `config` (its default shape, per-GPU
+    tuples, scaling as the main line) timed exactly like `value` -- a.warmup untimed launches, then
+    a.steps launches between barriers + synchronize, max over ranks -- with its roofline fraction
+    and every rank's self-check. Reported beside `value`, never as it."""
+    w = W.CONFIGS[config](local)
+    e = w.engine
+    base, n = shard_of(argparse.Namespace(**dict(vars(a), tuples=0)), w, rank, world)
+    b = D.TupleBatch(n, with_sport=(w.mode == 2))
+    D.gen_tuples(e, b, index_base=base, **w.gen)
+    out = torch.empty(n, dtype=torch.int32, device="cuda")
+    cptr = torch.zeros(e.num_counter_slots(), dtype=torch.int64, device="cuda") if w.counters else None
+    torch.cuda.synchronize()
+    for _ in range(a.warmup):
+        D.classify(e, w.mode, w.table_id, b, out, counters=cptr)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    if launched:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ev0.record()
+    for _ in range(a.steps):
+        D.classify(e, w.mode, w.table_id, b, out, counters=cptr)
+    ev1.record()
+    torch.cuda.synchronize()
+    if launched:
+        dist.barrier()
+    torch.cuda.synchronize()
+    wall = VD.max_over_ranks(time.perf_counter() - t0, "cuda")
+    kern_ms = ev0.elapsed_time(ev1) / a.steps
+    bpt, fields = bytes_per_tuple(w)
+    achieved = n * bpt / (kern_ms * 1e-3) / 1e9
+    traffic, traffic_src = pmc_traffic("%d" % config, n, False)
+    res = {"note": "side block: timed like `value` (%d warm-ups, %d steps), not the bench value" % (a.warmup, a.steps),
+           "workload": "config%d: %s" % (config, w.desc), "mode": MODE_NAME[w.mode], "counters": bool(w.counters),
+           "tuples_per_gpu": n, "rules": w.stats()["rules"], "tables": w.stats()["tables"],
+           "value": round(VD.sum_over_ranks(n, "cuda") * a.steps / wall / 1e6, 1), "unit": "Mpps",
+           "ms_per_step": round(wall * 1e3 / a.steps, 4),
+           "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_src,
+                        "bytes_per_tuple": bpt, "fields": fields, "kernel_ms": round(kern_ms, 4)}}
+    if not a.no_check:
+        pars = VD.gather_objects(shard_check(w, b, out, base, a.check_tuples, check_threads))
+        res["parity_sample"] = {"ranks": world, "tuples": sum(p["tuples"] for p in pars),
+                                "bit_exact_action_and_rule_index": all(p["bit_exact_action_and_rule_index"]
+                                                                       for p in pars),
+                                "counters_equal_oracle_histogram": all(p["counters_equal_oracle_histogram"]
+                                                                       for p in pars)}
+    return res
 
 
 def steady_state(e, w, b, out, cptr, n, world, settle=60, timed=20):
@@ -478,9 +541,10 @@ def cpu_baseline(w, b, out, k_max, faithful_s=8.0, budget_s=10.0):
     """The oracle's evalACL / testConnection (oracle/oracle.c, rules pre-parsed: BASELINE.md's
     B2) timed on this host's cores -- at one thread and at every core the process may use --
     over the first tuples of the same workload, each sample sized by a calibration run to
-    about budget_s (one thread: half of it); in SINGLE mode also the reference-faithful variant
-    (CIDR strings parsed on every rule visit, as evalACL does; one thread). The verdicts of
-    the multi-thread sample are compared with the GPU's."""
+    about budget_s (one thread: half of it); and the reference-faithful variant of the same call
+    (CIDR strings parsed on every rule visit, as evalACL does -- in every mode, so per-pod
+    evalACL and testConnection too; one thread). The verdicts of each sample are compared with
+    the GPU's."""
     from oracle import fast, world  # cpu_baseline leg: the checker, never the thing measured on GPU
 
     e = w.engine
@@ -510,6 +574,22 @@ def cpu_baseline(w, b, out, k_max, faithful_s=8.0, budget_s=10.0):
     rate_1, k_1, _ = _timed_rate(lambda k: run(k, 1), k_max, budget_s / 2, 4096)
     got = out[:k_n].cpu().numpy().view(np.uint32)
     ok = bool(((got >> 30) == res[0].astype(np.uint32)).all() and ((got & 0x3FFFFFFF) == to_slot(res)).all())
+    if w.mode != 0:
+        # the reference-faithful variant of the same call: every evalACL parses its rules' CIDR
+        # strings on each rule visit (aclengine_mock.go:535, 549), one thread
+        if w.mode == 1:
+            frun = lambda k: fast.perpod(wd.acls, wd.if_out, dif[:k], src[:k], dst[:k], dport[:k], proto[:k],
+                                         faithful=True)
+        else:
+            frun = lambda k: fast.test_connection(wd.acls, wd.if_in, wd.if_out, sif[:k], dif[:k], src[:k], dst[:k],
+                                                  sport[:k], dport[:k], proto[:k], faithful=True)
+        fr, kf, fres = _timed_rate(frun, k_max, faithful_s, 4096)
+        extra["faithful_1thread_mpps"] = round(fr / 1e6, 4)
+        extra["faithful_sample"] = kf
+        extra["faithful_kind"] = kind.replace("rules pre-parsed", "CIDR strings parsed per rule visit") + ", 1 thread"
+        extra["faithful_variant_bit_exact"] = bool(((got[:kf] >> 30) == fres[0].astype(np.uint32)).all() and
+                                                   ((got[:kf] & 0x3FFFFFFF) == to_slot(fres)).all()) \
+            if kf <= k_n else None
     if w.mode == 0:
         rules = e.GetACLByName(e.ACLNames()[w.table_id])["rules"]
         fr, kf, (fa, fi) = _timed_rate(lambda k: fast.eval_acl_faithful(rules, src[:k], dst[:k], dport[:k], proto[:k]),

@@ -155,7 +155,7 @@ int pg_ctx_device(const pg_ctx* ctx);
  * (PERPOD / CONN launches over a table set with more than 16382 slots: cells of the LDS cache the
  * hit counters go through -- the hottest slots of each workgroup's stream claim them, the rest
  * take global atomics -- rounded down to a power of two, up to 8192; default 256, < 16 = none);
- * table compiler (the context recompiles and re-uploads on its next use; hit counters restart)
+ * table compiler (the context recompiles and re-uploads on its next use; hit counters carry over)
  * -- "root_bits_max" (cap of the src/key trie root stride, 4..16, default 16), "node_build"
  * (1/0: build the node classifier for PERPOD / CONN, default 1), "node_root_bits" (its IPv4 /
  * key trie root stride cap, default 12), "lc_lds" (table blobs of at least this many words are
@@ -251,6 +251,12 @@ int pg_debug_classify_host(pg_ctx* ctx, int mode, int table_id, const pg_tuple_s
  * pg_debug_classify_host) as the LOCAL or CLUSTER snapshot in the currently compiled slot layout,
  * so the snapshot readers below can be tested without a GPU. n must equal the slot count. */
 int pg_debug_set_snapshot(pg_ctx* ctx, int which, const uint64_t* counters, size_t n);
+/* TESTS ONLY -- never on the classify path: the per-stream launch-mark bookkeeping of CONN launches
+ * (device.hpp StreamSlots, which pg_classify uses to hand a launch's deferred ANY-protocol packets
+ * to the k_conn_any launched after it on the same stream) replayed for n launches on the given
+ * stream handles: slot_out[k] = the mark word launch k writes, seq_out[k] = its launch number. No
+ * device work. */
+int pg_debug_stream_slots(const uint64_t* streams, size_t n, uint32_t* slot_out, uint32_t* seq_out);
 /* TESTS / MEASUREMENT ONLY -- never on the classify path: per tuple, the loads a SINGLE-mode
  * launch on table_id makes of the table's classification structure, split by where the launch
  * finds the word: lds_reads (the LDS-staged part) and mem_reads (HBM / L2 gathers; rule reads of
@@ -301,9 +307,13 @@ int pg_read_counters(pg_ctx* ctx, uint64_t* host_out, size_t n);
  *   PG_SNAP_CLUSTER  the sum over the communicator, as of the last pg_allreduce_counters*
  *   PG_SNAP_GAUGE    CLUSTER once the context has a communicator, else LOCAL: a monotonic
  *                    source either way (neither call writes the other's copy)
- * Slots are renumbered whenever the tables are recompiled (and the counters restart from
- * zero), so a gauge should be keyed by a stable rule identity -- (ACL name, rule index) -- and
- * read with pg_counter_of_rule, which resolves it in the snapshot's own layout. */
+ * Slots are renumbered whenever the tables are recompiled, so a gauge should be keyed by a
+ * stable rule identity -- (ACL name, rule index) -- and read with pg_counter_of_rule, which
+ * resolves it in the snapshot's own layout. Counts survive a recompile: every ACL present before
+ * and after it under the same name with the same rules keeps its counts (its rules and its
+ * default deny), as do "no ACL" and "unresolved" -- in the device counters (carried to the new
+ * slots when the new tables are uploaded) and in both host snapshots (when they are compiled);
+ * the slots of new or changed ACLs start at zero. */
 enum { PG_SNAP_GAUGE = 0, PG_SNAP_LOCAL = 1, PG_SNAP_CLUSTER = 2 };
 /* PG_SNAP_GAUGE snapshot: copies min(n, slots) -> number of slots in it (0 before the first read) */
 int pg_counters_snapshot(const pg_ctx* ctx, uint64_t* host_out, size_t n);
@@ -318,7 +328,7 @@ int pg_counters_snapshot_range(const pg_ctx* ctx, int which, uint32_t first, uin
 int pg_counter_of_rule(const pg_ctx* ctx, int which, const char* acl_name, int rule_index, uint64_t* value,
                        uint64_t* layout_gen);
 /* generation of the compiled slot layout (increments on every recompile; 0 = never compiled):
- * an agent re-registers gauges for new (ACL, rule) identities when it changes */
+ * an agent re-registers gauges for new (ACL, rule) identities when it changes. Any thread. */
 uint64_t pg_counter_layout_gen(const pg_ctx* ctx);
 
 /* ---- RCCL over xGMI: per-rule hit counters summed over the GPUs of a node -------------

@@ -31,6 +31,8 @@ def _load():
     lib.ora_eval.argtypes = [P, P, P, P, P, C.c_size_t, P, P, C.c_int]
     lib.ora_conn.argtypes = [P, P, P, P, P, P, P, P, P, P, C.c_size_t, P, P, P, P, P, C.c_int]
     lib.ora_perpod.argtypes = [P, P, P, P, P, P, P, C.c_size_t, P, P, P, C.c_int]
+    lib.ora_conn_faithful.argtypes = [P, P, P, P, P, P, P, P, P, P, C.c_size_t, P, P, P]
+    lib.ora_perpod_faithful.argtypes = [P, P, P, P, P, P, P, C.c_size_t, P, P, P]
     return lib
 
 
@@ -65,6 +67,15 @@ def rules_from_dicts(rules):
                     setattr(x, name + "_dst_lo", sec["dst"][0])
                     setattr(x, name + "_dst_hi", sec["dst"][1])
     return arr, keep
+
+
+class ora_facl(C.Structure):
+    _fields_ = [("r", C.POINTER(ora_rule)), ("n", C.c_int32)]
+
+
+def _facls(acls):
+    """the raw (string) rules of every table, for the faithful variants"""
+    return (ora_facl * max(1, len(acls)))(*[ora_facl(a.arr, a.n) for a in acls])
 
 
 class OraACL:
@@ -105,12 +116,14 @@ def eval_acl_faithful(rules_dicts, src, dst, dport, proto):
 
 
 def test_connection(acls, if_in, if_out, sif, dif, src, dst, sport, dport, proto, threads=os.cpu_count() or 1,
-                    trace=False):
+                    trace=False, faithful=False):
     """testConnection per tuple over resolved interfaces. acls: list of OraACL (table id order).
     Returns (ConnAction, last evaluated table (-1 none/-2 unresolved), last matched index);
     trace=True also returns every evaluation the connection made, in the order
     aclengine_mock.go:448-491 makes them: (tables int32[n, 4], indices int32[n, 4]), table -3 =
-    no evaluation, -2 = the unresolved-interface FAILURE, -1 = no ACL (nil: PERMIT)."""
+    no evaluation, -2 = the unresolved-interface FAILURE, -1 = no ACL (nil: PERMIT).
+    faithful=True: every evalACL parses its rules' CIDR strings on each rule visit, as
+    aclengine_mock.go:535, 549 do (one thread; no trace)."""
     n = len(src)
     harr = (C.c_void_p * max(1, len(acls)))(*[a.h for a in acls])
     cv = lambda a, dt: np.ascontiguousarray(a, dt)
@@ -118,6 +131,11 @@ def test_connection(acls, if_in, if_out, sif, dif, src, dst, sport, dport, proto
     src, dst, sport, dport, proto = (cv(src, np.uint32), cv(dst, np.uint32), cv(sport, np.uint16),
                                      cv(dport, np.uint16), cv(proto, np.uint8))
     conn, lt, li = np.empty(n, np.int32), np.empty(n, np.int32), np.empty(n, np.int32)
+    if faithful:
+        fa = _facls(acls)
+        lib.ora_conn_faithful(C.cast(fa, C.c_void_p), _p(if_in), _p(if_out), _p(sif), _p(dif), _p(src), _p(dst),
+                              _p(sport), _p(dport), _p(proto), n, _p(conn), _p(lt), _p(li))
+        return conn, lt, li
     evt = evi = None
     if trace:
         evt, evi = np.empty((n, 4), np.int32), np.empty((n, 4), np.int32)
@@ -129,15 +147,21 @@ def test_connection(acls, if_in, if_out, sif, dif, src, dst, sport, dport, proto
     return conn, lt, li
 
 
-def perpod(acls, if_out, dif, src, dst, dport, proto, threads=os.cpu_count() or 1):
+def perpod(acls, if_out, dif, src, dst, dport, proto, threads=os.cpu_count() or 1, faithful=False):
     """evalACL(outbound ACL of the dst interface) per tuple. Returns (ACLAction, table
-    (-1 = no ACL, -2 = unresolved interface), matched index (-1 = none))."""
+    (-1 = no ACL, -2 = unresolved interface), matched index (-1 = none)). faithful=True: CIDR
+    strings parsed on each rule visit (aclengine_mock.go:535, 549), one thread."""
     n = len(src)
     harr = (C.c_void_p * max(1, len(acls)))(*[a.h for a in acls])
     cv = lambda a, dt: np.ascontiguousarray(a, dt)
     if_out, dif = cv(if_out, np.int32), cv(dif, np.int32)
     src, dst, dport, proto = cv(src, np.uint32), cv(dst, np.uint32), cv(dport, np.uint16), cv(proto, np.uint8)
     act, lt, li = np.empty(n, np.int32), np.empty(n, np.int32), np.empty(n, np.int32)
+    if faithful:
+        fa = _facls(acls)
+        lib.ora_perpod_faithful(C.cast(fa, C.c_void_p), _p(if_out), _p(dif), _p(src), _p(dst), _p(dport), _p(proto),
+                                n, _p(act), _p(lt), _p(li))
+        return act, lt, li
     lib.ora_perpod(C.cast(harr, C.c_void_p), _p(if_out), _p(dif), _p(src), _p(dst), _p(dport), _p(proto), n,
                    _p(act), _p(lt), _p(li), threads)
     return act, lt, li

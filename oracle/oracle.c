@@ -7,7 +7,10 @@
  *                                visit exactly like the Go loop; ora_eval: same loop over
  *                                rules parsed once per ACL, multi-threaded)
  *   testConnection   :424-501   (ora_conn; optionally every evaluation it makes, in order:
- *                                the hit-counter histogram of a connection batch)
+ *                                the hit-counter histogram of a connection batch;
+ *                                ora_conn_faithful / ora_perpod_faithful: testConnection and
+ *                                the per-pod evalACL over ora_eval_faithful's string-parsing
+ *                                rule loop, the reference-shaped CPU baseline of those modes)
  * and Go 1.11 net.ParseCIDR / IPNet.Contains for IPv4 packets (src/net/ip.go), which the
  * evalACL loop calls per rule visit.  Independent of the product code in vpp_amd/csrc.
  * Pinned through oracle/aclengine.py (itself pinned by the reference's KATs) by
@@ -27,6 +30,11 @@ typedef struct {
     uint32_t tcp_src_lo, tcp_src_hi, tcp_dst_lo, tcp_dst_hi;
     uint32_t udp_src_lo, udp_src_hi, udp_dst_lo, udp_dst_hi;
 } ora_rule;
+
+typedef struct {  /* the raw rules of one ACL (the faithful variants) */
+    const ora_rule* r;
+    int n;
+} ora_facl;
 
 enum { A_DENY = 0, A_PERMIT = 1, A_REFLECT = 2, A_FAILURE = 3 };
 enum { P_TCP = 0, P_UDP = 1, P_OTHER = 2 };
@@ -333,7 +341,18 @@ typedef struct {
     int32_t *conn, *last_table, *last_idx;
     int32_t *ev_table, *ev_idx; /* optional: every evaluation, 4 per tuple (-3 = none) */
     size_t lo, hi;
+    const ora_facl* facls;      /* set: the reference-faithful evaluation (strings parsed per
+                                   rule visit) of these raw rules instead of acls */
 } conn_job;
+
+/* one evalACL of table t (-1 = nil ACL: PERMIT, aclengine_mock.go:506-508) */
+static inline int eval_tab(const conn_job* j, int32_t t, uint32_t x, uint32_t y, int pr, uint32_t port, int32_t* li) {
+    if (j->facls) {
+        if (t < 0) { *li = -1; return A_PERMIT; }
+        return eval_faithful_one(j->facls[t].r, j->facls[t].n, x, y, pr, port, li);
+    }
+    return eval_one(t >= 0 ? j->acls[t] : NULL, x, y, pr, port, li);
+}
 
 /* Every evalACL a connection makes is recorded in order (ev_table/ev_idx, up to 4 per
  * tuple, -3 = not made) when the caller asks for it: the per-rule hit counters of
@@ -359,7 +378,7 @@ static int conn_one(const conn_job* j, size_t i, int32_t* lt, int32_t* li) {
     do {                                                                         \
         int32_t t_ = (tab);                                                      \
         *lt = t_;                                                                \
-        a = eval_one(t_ >= 0 ? j->acls[t_] : NULL, x, y, pr, port, li);          \
+        a = eval_tab(j, t_, x, y, pr, port, li);                                 \
         if (evt) evt[nev] = t_, evi[nev] = *li;                                  \
         nev++;                                                                   \
     } while (0)
@@ -406,7 +425,7 @@ int ora_conn(const ora_acl* const* acls, const int32_t* if_in, const int32_t* if
         size_t lo = t * per, hi = (t + 1) * per < n ? (t + 1) * per : n;
         if (lo > hi) lo = hi;
         jobs[t] = (conn_job){acls, if_in, if_out, sif, dif, src, dst, sport, dport, proto, out_conn, out_last_table,
-                             out_last_idx, ev_table, ev_idx, lo, hi};
+                             out_last_idx, ev_table, ev_idx, lo, hi, NULL};
         pthread_create(&th[t], NULL, conn_worker, &jobs[t]);
     }
     for (int t = 0; t < threads; t++) pthread_join(th[t], NULL);
@@ -424,8 +443,7 @@ static void* perpod_worker(void* p) {
         }
         const int32_t t = j->if_out[di];
         j->last_table[i] = t;
-        j->conn[i] = eval_one(t >= 0 ? j->acls[t] : NULL, j->src[i], j->dst[i], j->proto[i], j->dport[i],
-                              &j->last_idx[i]);
+        j->conn[i] = eval_tab(j, t, j->src[i], j->dst[i], j->proto[i], j->dport[i], &j->last_idx[i]);
     }
     return NULL;
 }
@@ -442,9 +460,31 @@ int ora_perpod(const ora_acl* const* acls, const int32_t* if_out, const int32_t*
         size_t lo = t * per, hi = (t + 1) * per < n ? (t + 1) * per : n;
         if (lo > hi) lo = hi;
         jobs[t] = (conn_job){acls, NULL, if_out, NULL, dif, src, dst, NULL, dport, proto, out_action, out_table,
-                             out_idx, NULL, NULL, lo, hi};
+                             out_idx, NULL, NULL, lo, hi, NULL};
         pthread_create(&th[t], NULL, perpod_worker, &jobs[t]);
     }
     for (int t = 0; t < threads; t++) pthread_join(th[t], NULL);
+    return 0;
+}
+
+/* ---------------- the same, reference-faithful: CIDR strings parsed on every rule visit ----------
+ * (evalACL as aclengine_mock.go:535, 549 runs it: net.ParseCIDR per rule per packet), over the raw
+ * rules of every table; single-threaded by intent (the reference-shaped CPU baseline). */
+int ora_conn_faithful(const ora_facl* facls, const int32_t* if_in, const int32_t* if_out, const int32_t* sif,
+                      const int32_t* dif, const uint32_t* src, const uint32_t* dst, const uint16_t* sport,
+                      const uint16_t* dport, const uint8_t* proto, size_t n, int32_t* out_conn,
+                      int32_t* out_last_table, int32_t* out_last_idx) {
+    conn_job j = {NULL, if_in, if_out, sif, dif, src, dst, sport, dport, proto, out_conn, out_last_table,
+                  out_last_idx, NULL, NULL, 0, n, facls};
+    conn_worker(&j);
+    return 0;
+}
+
+int ora_perpod_faithful(const ora_facl* facls, const int32_t* if_out, const int32_t* dif, const uint32_t* src,
+                        const uint32_t* dst, const uint16_t* dport, const uint8_t* proto, size_t n,
+                        int32_t* out_action, int32_t* out_table, int32_t* out_idx) {
+    conn_job j = {NULL, NULL, if_out, NULL, dif, src, dst, NULL, dport, proto, out_action, out_table, out_idx,
+                  NULL, NULL, 0, n, facls};
+    perpod_worker(&j);
     return 0;
 }

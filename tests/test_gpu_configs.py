@@ -303,6 +303,74 @@ def test_rccl_counter_allreduce_single_rank():
     assert int(s2.sum()) == b.n
 
 
+def test_counters_survive_a_commit():
+    """Device hit counters across Commits (statscollector gauge, plugin_impl_statscollector.go:
+    248-261): count, commit a change to another ACL, count again -- the unchanged ACL's counts
+    (rules and default deny, read back and through its gauge) are the sum of both passes, the
+    changed ACL's only the second pass's. Three shapes of recompile: more slots (a new ACL), the
+    same slot count (one rule's action flipped: remapped in place), nothing changed (a compiler
+    knob: the counters stay where they are)."""
+    import acl_fuzz as fz
+    rnd = random.Random(21)
+    acls = {"b": fz.rand_acl(rnd, 60, fz.ANCHORS, weird=False, tail="deny"),
+            "d": fz.rand_acl(rnd, 40, fz.ANCHORS, weird=False, tail="permit")}
+    e = R.Engine(0)
+    e.SetMainInterfaceName("GbE")
+
+    def apply(a):
+        e.ApplyTxn(True, [("config/vpp/acls/v2/acl/" + n, {"name": n, "rules": r, "ingress": [], "egress": ["if-" + n]})
+                          for n, r in a.items()])
+
+    apply(acls)
+    tup = fz.rand_tuples(np.random.default_rng(21), 200000, fz.ANCHORS, any_pct=0.01)
+    b = D.TupleBatch.from_numpy(*tup)
+    out = torch.empty(b.n, dtype=torch.int32, device="cuda")
+
+    def count(names):  # one counted pass per table into the context's counters -> this pass's histogram
+        h = np.zeros(e.num_counter_slots(), np.int64)
+        for n in names:
+            D.classify(e, MODE_SINGLE, e.table_id(n), b, out, counters=D.counters_device_ptr(e))
+            torch.cuda.synchronize()
+            h += np.bincount(out.cpu().numpy().view(np.uint32) & 0x3FFFFFFF, minlength=len(h))
+        return h
+
+    def acl_slots(n):
+        base, nr, dflt = e.table_info(e.table_id(n))
+        return list(range(base, base + nr)) + [dflt]
+
+    D.reset_counters(e)
+    h1 = count(["b", "d"])
+    assert np.array_equal(D.read_counters(e), h1)
+    b1 = h1[acl_slots("b")]
+    # 1: a new ACL sorted first (every slot moves, more slots) and d changed (a rule dropped)
+    acls2 = {"a": fz.rand_acl(rnd, 30, fz.ANCHORS, weird=False, tail="deny"), "b": acls["b"], "d": acls["d"][1:]}
+    apply(acls2)
+    h2 = count(["a", "b", "d"])
+    got = D.read_counters(e)
+    assert np.array_equal(got[acl_slots("b")], b1 + h2[acl_slots("b")])
+    assert np.array_equal(got[acl_slots("d")], h2[acl_slots("d")])
+    assert np.array_equal(got[acl_slots("a")], h2[acl_slots("a")])
+    ns = e.num_counter_slots()
+    assert got[ns - 2] == h1[len(h1) - 2] + h2[ns - 2] and got[ns - 1] == h1[len(h1) - 1] + h2[ns - 1]
+    for i, s in enumerate(acl_slots("b")[:-1]):
+        assert D.counter_of_rule(e, _capi.SNAP_GAUGE, "b", i)[0] == got[s]
+    assert D.counter_of_rule(e, _capi.SNAP_GAUGE, "b", -1)[0] == got[acl_slots("b")[-1]]
+    # 2: the same slot count (d's first rule's action flipped): b and a carried, d restarts
+    d3 = [dict(r) for r in acls2["d"]]
+    d3[0]["action"] = 0 if d3[0]["action"] == 1 else 1
+    apply(dict(acls2, d=d3))
+    assert e.num_counter_slots() == ns
+    h3 = count(["b", "d"])
+    got3 = D.read_counters(e)
+    assert np.array_equal(got3[acl_slots("b")], got[acl_slots("b")] + h3[acl_slots("b")])
+    assert np.array_equal(got3[acl_slots("a")], got[acl_slots("a")])
+    assert np.array_equal(got3[acl_slots("d")], h3[acl_slots("d")])
+    # 3: a compiler knob (recompiled, nothing changed): every count stays
+    e.set_tuning("fd", 0)
+    h4 = count(["b"])
+    assert np.array_equal(D.read_counters(e), got3 + h4)
+
+
 # ---- rule-count sweep: gen-policy-shaped tables of 10k / 100k rules and the whole policy ----
 @pytest.mark.parametrize("n_rules", [10000, 100000])
 def test_rule_count_sweep_tables_bit_exact(n_rules):

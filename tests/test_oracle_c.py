@@ -83,3 +83,29 @@ def _acl_dicts(acl):
                 d[f] = {"src": [s.src_range.lower, s.src_range.upper], "dst": [s.dst_range.lower, s.dst_range.upper]}
         out.append(d)
     return out
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_faithful_conn_and_perpod_equal_the_preparsed_ones(seed):
+    """The reference-faithful testConnection / per-pod evalACL (CIDR strings parsed per rule
+    visit, aclengine_mock.go:535, 549; bench.py's reference-shaped CPU baseline of configs 3 and 5)
+    give the pre-parsed oracle's verdicts, tables and indices on random topologies: weird rules,
+    nil ACLs, unresolved interfaces, every protocol."""
+    rnd = random.Random(100 + seed)
+    rng = np.random.default_rng(seed)
+    acls = [fast.OraACL(fz.rand_acl(rnd, rnd.randint(1, 30), fz.ANCHORS, weird=True,
+                                    tail=rnd.choice([None, "deny", "permit"]))) for _ in range(5)]
+    n_if = 7
+    if_in = rng.integers(-1, len(acls), n_if).astype(np.int32)
+    if_out = rng.integers(-1, len(acls), n_if).astype(np.int32)
+    src, dst, sport, dport, proto = fz.rand_tuples(rng, 5000, fz.ANCHORS, any_pct=0.05)
+    sif = rng.integers(-1, n_if, len(src)).astype(np.int32)
+    dif = rng.integers(-1, n_if, len(src)).astype(np.int32)
+    ref = fast.test_connection(acls, if_in, if_out, sif, dif, src, dst, sport, dport, proto, threads=2)
+    got = fast.test_connection(acls, if_in, if_out, sif, dif, src, dst, sport, dport, proto, faithful=True)
+    for r, g in zip(ref, got):
+        assert np.array_equal(r, g)
+    ref = fast.perpod(acls, if_out, dif, src, dst, dport, proto, threads=2)
+    got = fast.perpod(acls, if_out, dif, src, dst, dport, proto, faithful=True)
+    for r, g in zip(ref, got):
+        assert np.array_equal(r, g)

@@ -96,9 +96,10 @@ def test_snapshot_reads_by_rule_identity_across_a_recompile():
     base_b_new = e.table_info(e.table_id("b"))[0]
     base_b_old = 0
     assert base_b_new != base_b_old
-    # the old snapshot still answers by identity in its own layout (and says which)
-    assert _by_rule(e, SNAP_GAUGE, "b", 3) == (int(cnt[3]), gen1)
-    assert _by_rule(e, SNAP_GAUGE, "a", 0) is None  # not in that layout
+    # the snapshot followed the recompile: unchanged ACLs answer with their counts in the new
+    # layout (and say which), the new ACL with zero
+    assert _by_rule(e, SNAP_GAUGE, "b", 3) == (int(cnt[3]), gen2)
+    assert _by_rule(e, SNAP_GAUGE, "a", 0) == (0, gen2)
     _set(e, SNAP_LOCAL, cnt2)
     assert _by_rule(e, SNAP_GAUGE, "a", 0) == (int(cnt2[e.table_info(e.table_id("a"))[0]]), gen2)
     assert _by_rule(e, SNAP_GAUGE, "b", 3) == (int(cnt2[base_b_new + 3]), gen2)
@@ -150,3 +151,124 @@ def test_snapshot_api_rejects_bad_arguments():
     assert lib.pg_counters_snapshot_range(e.h, 9, 0, 1, p, None) == _capi.PG_EINVAL
     with pytest.raises(Exception):
         _by_rule(e, SNAP_LOCAL, "x", -3)
+
+
+def _apply(e, acls):
+    e.ApplyTxn(True, [("config/vpp/acls/v2/acl/" + n, {"name": n, "rules": r, "ingress": [], "egress": ["if-" + n]})
+                      for n, r in acls.items()])
+
+
+def test_counts_survive_a_commit_that_changes_another_acl():
+    """A Commit that changes one ACL keeps every other ACL's counts (rules and default deny),
+    and "no ACL" / "unresolved"; the changed ACL starts at zero, a removed one is gone
+    (plugin_impl_statscollector.go:248-261: the gauge is a monotonic source)."""
+    import random
+    rnd = random.Random(11)
+    acls = {"b": fz.rand_acl(rnd, 40, fz.ANCHORS, weird=False, tail="deny"),
+            "d": fz.rand_acl(rnd, 25, fz.ANCHORS, weird=False, tail="permit"),
+            "f": fz.rand_acl(rnd, 10, fz.ANCHORS, weird=False, tail="deny")}
+    e = _engine(acls)
+    cnt = _classify_counts(e, "b", 1) + _classify_counts(e, "d", 2) + _classify_counts(e, "f", 3)
+    ns = len(cnt)
+    cnt[ns - 2] += 7  # "no ACL"
+    cnt[ns - 1] += 5  # "unresolved"
+    _set(e, SNAP_LOCAL, cnt)
+    _set(e, SNAP_CLUSTER, cnt * np.uint64(3))
+    old = {n: e.table_info(e.table_id(n)) for n in acls}
+    # d's rules change (one rule dropped), f is removed, a (sorted first) is added
+    acls2 = {"a": fz.rand_acl(rnd, 30, fz.ANCHORS, weird=False, tail="deny"), "b": acls["b"], "d": acls["d"][1:]}
+    _apply(e, acls2)
+    e.num_counter_slots()  # compiles the new layout (no device)
+    gen = lib.pg_counter_layout_gen(e.h)
+    base, n, dflt = old["b"]
+    for which, k in ((SNAP_LOCAL, 1), (SNAP_CLUSTER, 3)):
+        for i in range(n):
+            assert _by_rule(e, which, "b", i) == (int(cnt[base + i]) * k, gen)
+        assert _by_rule(e, which, "b", -1) == (int(cnt[dflt]) * k, gen)
+        for i in range(len(acls2["d"])):
+            assert _by_rule(e, which, "d", i) == (0, gen)
+        assert _by_rule(e, which, "d", -1) == (0, gen)
+        assert _by_rule(e, which, "a", 0) == (0, gen)
+        assert _by_rule(e, which, "f", 0) is None
+        assert _by_rule(e, which, None, -1) == (int(cnt[ns - 2]) * k, gen)
+        assert _by_rule(e, which, None, -2) == (int(cnt[ns - 1]) * k, gen)
+    # the whole snapshot is in the new layout
+    ns2 = e.num_counter_slots()
+    v, g = _range(e, SNAP_LOCAL, 0, ns2)
+    assert g == gen and len(v) == ns2
+    nb, _, db = e.table_info(e.table_id("b"))
+    assert np.array_equal(v[nb:nb + n], cnt[base:base + n]) and v[db] == cnt[dflt]
+    assert int(v.sum()) == int(cnt[base:base + n].sum() + cnt[dflt] + cnt[ns - 2] + cnt[ns - 1])
+    # a recompile that changes nothing (a compiler knob) keeps every count
+    e.set_tuning("fd", 0)
+    e.num_counter_slots()
+    assert lib.pg_counter_layout_gen(e.h) > gen
+    v2, _ = _range(e, SNAP_LOCAL, 0, ns2)
+    assert np.array_equal(v2, v)
+    # same name, same rule count, one rule's action flipped: a changed ACL
+    b2 = [dict(r) for r in acls2["b"]]
+    b2[0]["action"] = 1 - b2[0]["action"] if b2[0]["action"] in (0, 1) else 0
+    _apply(e, dict(acls2, b=b2))
+    e.num_counter_slots()
+    assert _by_rule(e, SNAP_LOCAL, "b", 1)[0] == 0
+
+
+def test_layout_generation_polled_during_recompiles():
+    """pg_counter_layout_gen from other threads while the control thread recompiles (an atomic;
+    the TSan build runs this too): it only ever increases"""
+    import random
+    rnd = random.Random(5)
+    acls = {"x": fz.rand_acl(rnd, 30, fz.ANCHORS, weird=False, tail="deny")}
+    e = _engine(acls)
+    e.num_counter_slots()
+    stop = threading.Event()
+    bad = []
+
+    def poll():
+        last = 0
+        while not stop.is_set():
+            g = lib.pg_counter_layout_gen(e.h)
+            if g < last:
+                bad.append((last, g))
+            last = g
+
+    th = [threading.Thread(target=poll) for _ in range(2)]
+    for t in th:
+        t.start()
+    for k in range(20):
+        e.set_tuning("fd", k % 2)
+        e.num_counter_slots()
+    stop.set()
+    for t in th:
+        t.join()
+    assert not bad
+
+
+def test_stream_slot_bookkeeping():
+    """CONN launches hand their deferred ANY-protocol packets to the k_conn_any after them on the
+    same stream through a per-(table set, stream) mark word (device.hpp StreamSlots): one slot per
+    stream, launch numbers strictly increasing and never 0 per slot, and numbers never repeated
+    at a slot across a drain (clear) that reassigns slots to other streams."""
+    rng = np.random.default_rng(1)
+    streams = rng.integers(1, 80, size=3000).astype(np.uint64)  # 79 streams > 32 slots: drains
+    streams[:40] = 0  # the null stream too
+    n = len(streams)
+    slot, seq = (C.c_uint32 * n)(), (C.c_uint32 * n)()
+    assert lib.pg_debug_stream_slots(streams.ctypes.data_as(C.POINTER(C.c_uint64)), n, slot, seq) == 0
+    slot, seq = np.frombuffer(slot, np.uint32), np.frombuffer(seq, np.uint32)
+    assert slot.max() < 32 and seq.min() > 0
+    # model: a stream keeps its slot until a drain; a drain happens only when a 33rd stream
+    # arrives, and empties every slot
+    live, last, drains = [], {}, 0
+    for s, i, q in zip(streams.tolist(), slot.tolist(), seq.tolist()):
+        if s not in live:
+            if len(live) == 32:
+                live, drains = [], drains + 1
+            live.append(s)
+        assert i == live.index(s)  # one slot per live stream, distinct across streams
+        assert q > last.get(i, 0)  # per slot strictly increasing, across drains too
+        last[i] = q
+    assert drains > 10
+    # the first 40 launches, all on the null stream: one slot, numbers 1..40
+    assert set(slot[:40]) == {0} and np.array_equal(seq[:40], np.arange(1, 41))
+    assert lib.pg_debug_stream_slots(None, 0, None, None) == 0

@@ -123,6 +123,8 @@ _SIGS = {
     "pg_counter_of_rule": (C.c_int, [_P, C.c_int, C.c_char_p, C.c_int, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
     "pg_counter_layout_gen": (C.c_uint64, [_P]),
     "pg_debug_set_snapshot": (C.c_int, [_P, C.c_int, C.POINTER(C.c_uint64), C.c_size_t]),
+    "pg_debug_stream_slots": (C.c_int, [C.POINTER(C.c_uint64), C.c_size_t, C.POINTER(C.c_uint32),
+                                        C.POINTER(C.c_uint32)]),
     "pg_comm_unique_id": (C.c_int, [C.c_char_p]),
     "pg_comm_init_rank": (C.c_int, [_P, C.c_int, C.c_char_p, C.c_int]),
     "pg_comm_init_all": (C.c_int, [C.POINTER(_P), C.c_int]),

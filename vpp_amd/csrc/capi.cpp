@@ -717,6 +717,23 @@ int pg_debug_set_snapshot(pg_ctx* ctx, int which, const uint64_t* counters, size
     GUARD_END(ctx)
 }
 
+int pg_debug_stream_slots(const uint64_t* streams, size_t n, uint32_t* slot_out, uint32_t* seq_out) {
+    if ((!streams || !slot_out || !seq_out) && n) return PG_EINVAL;
+    StreamSlots S;  // what dev_any_mark does per launch, without the events and the device words
+    for (size_t k = 0; k < n; k++) {
+        const void* s = (const void*)(uintptr_t)streams[k];
+        size_t i = 0;
+        bool added = false;
+        if (!S.slot(s, &i, &added)) {  // (device.hip use_slot: drains the recorded launches first)
+            S.clear();
+            S.slot(s, &i, &added);
+        }
+        slot_out[k] = (uint32_t)i;
+        seq_out[k] = S.draw(i);
+    }
+    return PG_OK;
+}
+
 int pg_node_stats(pg_ctx* ctx, uint32_t* ip_classes, uint32_t* key_classes, uint64_t* image_bytes,
                   uint64_t* cross_bytes) {
     if (!ctx) return PG_EINVAL;
@@ -793,7 +810,11 @@ int pg_classify(pg_ctx* ctx, int mode, int table_id, const pg_tuple_soa* t, uint
     if (!t->src_ip || !t->dst_ip || !t->dst_port || !t->proto || (mode == PG_MODE_CONN && !t->src_port))
         return fail(ctx, PG_EINVAL, "missing tuple field");
     std::string err;
-    if (dev_classify(T, ctx->eng.tune, mode, table_id, t->src_ip, t->dst_ip, t->src_port, t->dst_port, t->proto, n,
+    DevTableSet TL = T;
+    // CONN: the launch stream's mark word and this launch's number (device.hpp StreamSlots)
+    if (mode == PG_MODE_CONN && !(TL.any_mark = dev_any_mark(ctx->eng.cur, stream, &TL.any_seq, &err)))
+        return fail(ctx, PG_EIO, err);
+    if (dev_classify(TL, ctx->eng.tune, mode, table_id, t->src_ip, t->dst_ip, t->src_port, t->dst_port, t->proto, n,
                      out, (unsigned long long*)counters, stream, &err) != 0 ||
         dev_mark_use(ctx->eng.cur, stream, counters != nullptr, &err) != 0)
         return fail(ctx, PG_EIO, err);
@@ -932,7 +953,8 @@ int pg_counter_of_rule(const pg_ctx* ctx, int which, const char* acl_name, int r
 
 uint64_t pg_counter_layout_gen(const pg_ctx* ctx) {
     if (!ctx) return 0;
-    return ctx->eng.layout ? ctx->eng.layout->gen : 0;
+    // (any thread: compile() publishes the generation after the layout and snapshots are in place)
+    return ctx->eng.layout_gen_pub.load(std::memory_order_acquire);
 }
 
 // ---- RCCL: per-rule hit counters summed over GPUs --------------------------
@@ -947,8 +969,12 @@ static int comm_attach(pg_ctx* ctx, void* comm, int rank, int nranks) {
     std::string err;
     if (!E.comm_check && !(E.comm_check = (unsigned long long*)dev_alloc(4 * 8, &err)))
         return fail(ctx, PG_ENOMEM, err);
-    if (E.comm) dev_comm_destroy(E.comm);
-    E.comm = comm;
+    void* old = E.comm;
+    {
+        std::lock_guard<std::mutex> lk(E.snap_mu);  // pick_snapshot reads E.comm under it
+        E.comm = comm;
+    }
+    if (old) dev_comm_destroy(old);
     E.comm_rank = rank;
     E.comm_nranks = nranks;
     return PG_OK;
@@ -988,8 +1014,12 @@ int pg_comm_init_all(pg_ctx* const* ctxs, int n) {
 int pg_comm_destroy(pg_ctx* ctx) {
     if (!ctx) return PG_EINVAL;
     DEVICE_GUARD(ctx);
-    if (ctx->eng.comm) dev_comm_destroy(ctx->eng.comm);
-    ctx->eng.comm = nullptr;
+    void* old = ctx->eng.comm;
+    {
+        std::lock_guard<std::mutex> lk(ctx->eng.snap_mu);  // pick_snapshot reads E.comm under it
+        ctx->eng.comm = nullptr;
+    }
+    if (old) dev_comm_destroy(old);
     ctx->eng.comm_rank = -1;
     ctx->eng.comm_nranks = 0;
     return PG_OK;

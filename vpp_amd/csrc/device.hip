@@ -51,11 +51,12 @@ struct DeviceBuffers {
     // launch on each: the set is freed (and counters read) once those have completed, without
     // a device-wide synchronisation (dev_mark_use)
     struct Use {
-        hipStream_t s;
         hipEvent_t plain, fenced;
         bool plain_rec, fenced_rec;
     };
-    std::vector<Use> uses;
+    std::vector<Use> uses;  // uses[i]: the stream of slot i (StreamSlots)
+    StreamSlots slots;
+    uint32_t* marks = nullptr;  // device: StreamSlots::kMax launch-mark words (CONN, k_conn_any)
 };
 
 const DevTableSet& dev_view(const DeviceBuffers* b) { return b->view; }
@@ -107,17 +108,11 @@ int dev_stream_sync(void* stream, std::string* err) {
 // others -- freeing a set needs only that its readers have finished, and a system-scope fence
 // per record cost ~3 us per back-to-back launch on MI355X (tools/gap_probe.py: 130.2 -> 127.1 us
 // per config-2 launch without it)
-int dev_mark_use(DeviceBuffers* b, void* stream, bool fenced, std::string* err) {
-    const hipStream_t s = (hipStream_t)stream;
-    for (auto& u : b->uses)
-        if (u.s == s) {
-            HIPCHK(hipEventRecord(fenced ? u.fenced : u.plain, s));
-            (fenced ? u.fenced_rec : u.plain_rec) = true;
-            return 0;
-        }
-    // bounded list: past kMaxUses streams, wait for the recorded launches and start over
-    constexpr size_t kMaxUses = 32;
-    if (b->uses.size() >= kMaxUses) {
+// The slot of `stream` (StreamSlots; its events created when new). Bounded: past kMax streams,
+// wait for every recorded launch and start over.
+static int use_slot(DeviceBuffers* b, hipStream_t s, size_t* i, std::string* err) {
+    bool added = false;
+    if (!b->slots.slot(s, i, &added)) {
         // wait for every recorded launch (keeping the first error), then destroy every event and
         // clear the list on both paths, so no destroyed event stays listed
         hipError_t first = hipSuccess;
@@ -131,18 +126,43 @@ int dev_mark_use(DeviceBuffers* b, void* stream, bool fenced, std::string* err) 
             (void)hipEventDestroy(u.fenced);
         }
         b->uses.clear();
+        b->slots.clear();
         if (first != hipSuccess) {
             if (err) *err = std::string("hipEventSynchronize: ") + hipGetErrorString(first);
             return -1;
         }
+        b->slots.slot(s, i, &added);
     }
-    DeviceBuffers::Use u{s, nullptr, nullptr, false, false};
-    HIPCHK(hipEventCreateWithFlags(&u.plain, hipEventDisableTiming | hipEventDisableSystemFence));
-    HIPCHK(hipEventCreateWithFlags(&u.fenced, hipEventDisableTiming));
-    b->uses.push_back(u);
-    HIPCHK(hipEventRecord(fenced ? u.fenced : u.plain, s));
-    (fenced ? b->uses.back().fenced_rec : b->uses.back().plain_rec) = true;
+    if (added) {
+        DeviceBuffers::Use u{nullptr, nullptr, false, false};
+        hipError_t e = hipEventCreateWithFlags(&u.plain, hipEventDisableTiming | hipEventDisableSystemFence);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&u.fenced, hipEventDisableTiming);
+        if (e != hipSuccess) {
+            if (u.plain) (void)hipEventDestroy(u.plain);
+            b->slots.streams.pop_back();  // (the slot just added: the lists stay aligned)
+            if (err) *err = std::string("hipEventCreateWithFlags: ") + hipGetErrorString(e);
+            return -1;
+        }
+        b->uses.push_back(u);
+    }
     return 0;
+}
+
+int dev_mark_use(DeviceBuffers* b, void* stream, bool fenced, std::string* err) {
+    const hipStream_t s = (hipStream_t)stream;
+    size_t i = 0;
+    if (use_slot(b, s, &i, err) != 0) return -1;
+    DeviceBuffers::Use& u = b->uses[i];
+    HIPCHK(hipEventRecord(fenced ? u.fenced : u.plain, s));
+    (fenced ? u.fenced_rec : u.plain_rec) = true;
+    return 0;
+}
+
+uint32_t* dev_any_mark(DeviceBuffers* b, void* stream, uint32_t* seq, std::string* err) {
+    size_t i = 0;
+    if (use_slot(b, (hipStream_t)stream, &i, err) != 0) return nullptr;
+    *seq = b->slots.draw(i);
+    return b->marks + i;
 }
 
 int dev_wait_uses(DeviceBuffers* b, std::string* err) {
@@ -169,6 +189,7 @@ DeviceBuffers* dev_upload(const HostTableSet& h, std::string* err) {
     size_t o_ip = place(h.iphash.size() * 4);
     size_t o_nimg = place(h.node_img.size() * 4);
     size_t o_nx = place(h.node_cross.size() * 4);
+    size_t o_mark = place(StreamSlots::kMax * 4);  // launch-mark words, zero
     std::vector<uint8_t> img(off, 0);
     auto put = [&](size_t o, const void* p, size_t n) {
         if (n) std::memcpy(img.data() + o, p, n);
@@ -212,6 +233,9 @@ DeviceBuffers* dev_upload(const HostTableSet& h, std::string* err) {
     v.node = h.node;
     v.node.img = h.node_img.empty() ? nullptr : (const uint32_t*)(base + o_nimg);
     v.node.cross = h.node_img.empty() ? nullptr : (const uint32_t*)(base + o_nx);
+    v.any_mark = nullptr;
+    v.any_seq = 0;
+    b->marks = (uint32_t*)(base + o_mark);
     b->host_tabs = h.tabs;
     b->host_blob_words = h.blob_words;
     b->host_blob_prefix = h.blob_prefix;
@@ -458,17 +482,13 @@ constexpr size_t kLdsPerCU = 160u << 10;
 // cost the kernel its SGPR allocation: 54 SGPRs spilled to VGPR lanes, a v_readlane per use;
 // a pass after the loop in the same kernel still cost 6 % (A/B on MI355X, config 5 with
 // counters: in-loop call 123, pass after the loop 129, no pass 137 Gpps; PERPOD unchanged by
-// any of it, so it keeps the call). A launch that deferred a packet marks its slot of a ring
-// with its sequence number; the k_conn_any launch of the same number classifies the batch's
-// ANY-protocol packets when it finds it, and returns at once otherwise.
+// any of it, so it keeps the call). A launch that deferred a packet writes its number into its
+// stream's mark word (device.hpp StreamSlots, DevTableSet any_mark / any_seq); the k_conn_any
+// launched after it on that stream classifies the batch's ANY-protocol packets when the word
+// holds its number, and returns at once otherwise -- stream order makes the word this launch's.
 #ifndef PG_CONN_DEFER_ANY
 #define PG_CONN_DEFER_ANY 1
 #endif
-constexpr uint32_t kAnySlots = 4096;  // (a power of two)
-__device__ uint32_t g_any_seq[kAnySlots];
-// launch numbers, one sequence for the process (every launch_bs instantiation draws from it:
-// concurrent launches must not share a ring slot with different numbers)
-static std::atomic<uint32_t> g_launch_seq{1};
 // any of the four protocol bytes of w above 2 (bytes >= 0x80 by their top bit, the rest by a
 // carry-free add into it)
 __device__ __forceinline__ bool any_proto_gt2(uint32_t w) {
@@ -478,9 +498,8 @@ __device__ __forceinline__ bool any_proto_gt2(uint32_t w) {
 template <bool COUNT>
 __global__ __launch_bounds__(kBlock) void k_conn_any(DevTableSet T, const uint32_t* __restrict__ src,
                                                   const uint32_t* __restrict__ dst, const uint8_t* __restrict__ proto,
-                                                  uint64_t n, uint32_t* __restrict__ out, unsigned long long* counters,
-                                                  uint32_t seq) {
-    if (g_any_seq[seq & (kAnySlots - 1u)] != seq) return;
+                                                  uint64_t n, uint32_t* __restrict__ out, unsigned long long* counters) {
+    if (*T.any_mark != T.any_seq) return;
     const Hist h{nullptr, counters};  // global increments (rare packets)
     const uint64_t stride = (uint64_t)gridDim.x * kBlock;
     for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride)
@@ -577,7 +596,7 @@ void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
                                                      const uint16_t* __restrict__ dport,
                                                      const uint8_t* __restrict__ proto, uint64_t n,
                                                      uint32_t* __restrict__ out, unsigned long long* counters,
-                                                     uint32_t stage_words, uint32_t hist_cells, uint32_t any_seq) {
+                                                     uint32_t stage_words, uint32_t hist_cells) {
     constexpr int STAGE = STAGE_ & 7;
     constexpr bool NODST = MODE == 0 && (STAGE_ & 8);
     // STAGE_ + 16 (node kernels with counters): the LDS histogram holds every slot (launcher)
@@ -715,13 +734,14 @@ void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
     // once after the first chunk's cross-entry loads are issued (node kernels, PF 2)
     auto run_group = [&](const Group& g, uint64_t qq, auto&& hk) {
         uint32_t sv[P], dv[P], spv[P], dpv[P], prv[P], o[P];
-        // (DEFER) a protocol code > 2 among the group's: mark this launch's ring slot for
-        // k_conn_any (one test of the packed protocol word per group, no state across groups)
+        // (DEFER) a protocol code > 2 among the group's: this launch's number into its stream's
+        // mark word for k_conn_any (one test of the packed protocol word per group, no state
+        // across groups)
         if constexpr (DEFER) {
             bool any = false;
 #pragma unroll
             for (int k = 0; k < P / 4; k++) any |= any_proto_gt2(g.pr.w[k]);
-            if (any) g_any_seq[any_seq & (kAnySlots - 1u)] = any_seq;
+            if (any) *T.any_mark = T.any_seq;
         }
 #pragma unroll
         for (int j = 0; j < P; j++) {
@@ -804,7 +824,7 @@ void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
         else if constexpr (NODE) classify_node_q<MODE, COUNT, 1, STAGE && PG_PRED, STAGE == 3, NOPAIR, UNIF, DEFER>(T, T.node, img, s1, d1, sp1, dp1, pr1, h, o);
         else classify_q<MODE, COUNT, 1, STAGE == 1 && PG_PRED>(T, blobs, tab0, s1, d1, sp1, dp1, pr1, h, o, rootb);
         out[i] = o[0];
-        if (DEFER && pr1[0] > 2u) g_any_seq[any_seq & (kAnySlots - 1u)] = any_seq;
+        if (DEFER && pr1[0] > 2u) *T.any_mark = T.any_seq;
     }
     // (the packets deferred above -- ANY protocol, rare -- are classified by k_conn_any, launched
     // after this kernel on the same stream)
@@ -1035,19 +1055,14 @@ static void launch_bs(const DevTableSet& T, const Tuning& tu, int t, const uint3
     // three times; with counters no difference): fewer streams in flight per CU contend less
     const uint32_t bpc = tu.blocks_per_cu ? tu.blocks_per_cu : (MODE == 0 && (STAGE & 7) == 4 && !COUNT ? 2u : 0u);
     const size_t lds = hist + (size_t)stage * 4;
-    // CONN over a uniform node: the launch's number for its deferred ANY-protocol packets, and
-    // k_conn_any after it (PG_CONN_DEFER_ANY)
+    // CONN over a uniform node: k_conn_any after the classify kernel, for its deferred
+    // ANY-protocol packets (PG_CONN_DEFER_ANY; the launch's mark word and number: dev_classify)
     constexpr bool defer = MODE == 2 && NODE && (STAGE & 32) && (STAGE & 64) && PG_CONN_DEFER_ANY;
-    uint32_t seq = 0;
-    if constexpr (defer) {
-        seq = g_launch_seq.fetch_add(1, std::memory_order_relaxed);
-        if (seq == 0) seq = g_launch_seq.fetch_add(1, std::memory_order_relaxed);  // (0: never written)
-    }
     hipLaunchKernelGGL(k, dim3(grid_resident(k, BS, lds, items, bpc)), dim3(BS), lds, st, T, t, src, dst, sport, dport,
-                       proto, n, out, counters, stage, cells, seq);
+                       proto, n, out, counters, stage, cells);
     if constexpr (defer)
         hipLaunchKernelGGL(k_conn_any<COUNT>, dim3(grid_for(n)), dim3(kBlock), 0, st, T, src, dst, proto, n, out,
-                           counters, seq);
+                           counters);
 }
 
 // Workgroup size: a staged image is shared by the workgroup, so larger workgroups hold more
@@ -1215,6 +1230,10 @@ int dev_classify(const DevTableSet& T, const Tuning& tu, int mode, int table_id,
                  const uint32_t* dst, const uint16_t* sport, const uint16_t* dport, const uint8_t* proto, uint64_t n,
                  uint32_t* out, unsigned long long* counters, void* stream, std::string* err) {
     if (n == 0) return 0;
+    if (mode == 2 && !T.any_mark) {  // (a CONN build may defer packets to k_conn_any: dev_any_mark)
+        if (err) *err = "CONN launch without a launch-mark word";
+        return -1;
+    }
     auto al = [](const void* p, uintptr_t a) { return ((uintptr_t)p & (a - 1)) == 0; };
     // the group loads: 4*P-byte src/dst/out (16-B pieces), 2*P-byte ports, P-byte protocols
     const uintptr_t P = mode == 2 ? tuples_per_lane<2>() : tuples_per_lane<0>();
@@ -1274,6 +1293,34 @@ int dev_gen(const DevTableSet& T, const GenParams& g, uint64_t n, uint32_t* src,
     hipLaunchKernelGGL(k_gen, dim3(grid_for(n)), dim3(kBlock), 0, (hipStream_t)stream, T, g, n, src, dst, sport,
                        dport, proto);
     HIPCHK(hipGetLastError());
+    return 0;
+}
+
+// hit counters carried into a recompiled set's slots (engine.cpp slot_remap)
+__global__ __launch_bounds__(kBlock) void k_counter_remap(unsigned long long* __restrict__ dst,
+                                                          const unsigned long long* __restrict__ src,
+                                                          const uint32_t* __restrict__ map, uint32_t n) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i < n) dst[i] = map[i] == 0xFFFFFFFFu ? 0ull : src[map[i]];
+}
+
+int dev_counters_remap(unsigned long long* dst, const unsigned long long* src, const uint32_t* map, size_t n,
+                       std::string* err) {
+    if (n == 0) return 0;
+    uint32_t* m = nullptr;
+    HIPCHK(hipMalloc(&m, n * 4));
+    hipError_t e = hipMemcpy(m, map, n * 4, hipMemcpyHostToDevice);
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(k_counter_remap, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, 0, dst, src,
+                           m, (uint32_t)n);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipStreamSynchronize(nullptr);  // (m is freed next)
+    (void)hipFree(m);
+    if (e != hipSuccess) {
+        if (err) *err = std::string("counter remap: ") + hipGetErrorString(e);
+        return -1;
+    }
     return 0;
 }
 

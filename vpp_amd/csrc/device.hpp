@@ -118,6 +118,36 @@ constexpr uint32_t kLdsHistCells = 16382;
 constexpr int32_t kEndRemote = 1 << 28, kEndInet = 2 << 28;
 constexpr uint32_t kEndKindShift = 28;
 
+// Streams that launched kernels reading one table set, one slot each (device.hip DeviceBuffers:
+// the slot's completion events, and its CONN launch-mark word). A CONN launch over a uniform node
+// defers its ANY-protocol packets to k_conn_any, launched after it on the same stream
+// (device.hip PG_CONN_DEFER_ANY): the classify kernel writes its launch number into its
+// stream's mark word when it deferred a packet, and k_conn_any runs only when the word holds its
+// own number. Both launches are on one stream, so stream order alone makes the mark the one of
+// this launch; a stale number (an earlier launch, or a slot reassigned after clear()) can only
+// equal a later launch's after 2^32 - 1 more draws, and then k_conn_any makes a pass that finds
+// nothing to do -- never a skipped packet. Host-only bookkeeping, tested without a GPU
+// (pg_debug_stream_slots).
+struct StreamSlots {
+    static constexpr size_t kMax = 32;  // slots; past this many streams the caller drains and clears
+    std::vector<const void*> streams;   // slot i serves streams[i]
+    uint32_t seq[kMax] = {};            // last launch number drawn at each slot (kept across clear())
+    // slot of stream s (added when unseen: *added); false when every slot serves another stream --
+    // the caller waits for the launches recorded at the slots, then clear()s
+    bool slot(const void* s, size_t* i, bool* added) {
+        for (size_t k = 0; k < streams.size(); k++)
+            if (streams[k] == s) return *i = k, *added = false, true;
+        if (streams.size() >= kMax) return false;
+        streams.push_back(s);
+        return *i = streams.size() - 1, *added = true, true;
+    }
+    uint32_t draw(size_t i) {  // the next launch number of slot i (never 0: a fresh mark word holds 0)
+        if (++seq[i] == 0) ++seq[i];
+        return seq[i];
+    }
+    void clear() { streams.clear(); }
+};
+
 struct DevTableSet {       // device pointers (valid on the GPU)
     const DevRule* rules;
     const DevTable* tabs;
@@ -138,6 +168,10 @@ struct DevTableSet {       // device pointers (valid on the GPU)
     // ACL", in a register
     uint32_t slot_hot_in;
     DevNode node;
+    // CONN launches: the launch stream's mark word and this launch's number (StreamSlots; set per
+    // launch by pg_classify through dev_any_mark, null otherwise)
+    uint32_t* any_mark;
+    uint32_t any_seq;
     const DevTable* host_tabs;       // host copies (launch decisions; not dereferenced on the GPU)
     const uint32_t* host_blob_words;
     const uint32_t* host_blob_prefix;  // FD blobs: words of the prefix a STAGE 5 launch stages
@@ -278,6 +312,12 @@ int dev_sync(std::string* err);
 int dev_stream_sync(void* stream, std::string* err);
 // record that `stream` launched kernels reading table set b (dev_free / dev_wait_uses wait for them)
 int dev_mark_use(DeviceBuffers* b, void* stream, bool fenced, std::string* err);
+// dst[i] = map[i] == kNoSlot (engine.hpp) ? 0 : src[map[i]] for n slots (map: host), on the null
+// stream (the caller synchronises)
+int dev_counters_remap(unsigned long long* dst, const unsigned long long* src, const uint32_t* map, size_t n,
+                       std::string* err);
+// the launch-mark word of `stream` for table set b and the next launch number at it (StreamSlots)
+uint32_t* dev_any_mark(DeviceBuffers* b, void* stream, uint32_t* seq, std::string* err);
 int dev_wait_uses(DeviceBuffers* b, std::string* err);
 // RCCL communicators (opaque ncclComm_t), librccl opened on first use
 int dev_comm_unique_id(uint8_t* id /* 128 B */, std::string* err);

@@ -162,6 +162,59 @@ DevRule compile_acl_rule(const AclRule& r) {
     return d;
 }
 
+// ---- counters across recompiles -----------------------------------------------------------
+uint64_t acl_rules_hash(const ACL& acl) {
+    uint64_t h = 1469598103934665603ull;
+    auto mix = [&](const void* p, size_t n) {
+        for (size_t i = 0; i < n; i++) h = (h ^ ((const uint8_t*)p)[i]) * 1099511628211ull;
+    };
+    auto u32 = [&](uint32_t v) { mix(&v, 4); };
+    auto str = [&](const std::string& s) { u32((uint32_t)s.size()), mix(s.data(), s.size()); };
+    auto l4 = [&](const L4Section& s) {
+        u32(s.present | s.has_src << 1 | s.has_dst << 2);
+        u32(s.src.lower), u32(s.src.upper), u32(s.dst.lower), u32(s.dst.upper);
+    };
+    u32((uint32_t)acl.rules.size());
+    for (const AclRule& r : acl.rules) {
+        u32((uint32_t)r.action);
+        u32(r.has_macip | r.has_ip_rule << 1 | r.has_ip << 2 | r.has_icmp << 3);
+        str(r.src_network), str(r.dst_network);
+        l4(r.tcp), l4(r.udp);
+    }
+    return h;
+}
+
+std::vector<uint32_t> slot_remap(const SlotLayout& from, const SlotLayout& to, bool* identity) {
+    std::vector<uint32_t> m(to.slots, kNoSlot);
+    for (const auto& kv : to.tabs) {
+        const auto it = from.tabs.find(kv.first);
+        if (it == from.tabs.end()) continue;
+        const SlotLayout::Tab &a = it->second, &b = kv.second;
+        if (a.n != b.n || a.rules_hash != b.rules_hash) continue;  // changed: starts at zero
+        for (uint32_t r = 0; r < b.n; r++) m[b.base + r] = a.base + r;
+        m[b.dflt] = a.dflt;
+    }
+    m[to.noacl] = from.noacl;
+    m[to.unresolved] = from.unresolved;
+    if (identity) {
+        bool id = from.slots == to.slots;
+        for (uint32_t s = 0; id && s < to.slots; s++) id = m[s] == s;
+        *identity = id;
+    }
+    return m;
+}
+
+// a snapshot's counts carried into layout L (the slots of changed / new ACLs read zero)
+static void remap_snapshot(CounterSnapshot& s, const std::shared_ptr<const SlotLayout>& L) {
+    if (!s.layout || s.layout == L) return;
+    const std::vector<uint32_t> m = slot_remap(*s.layout, *L);
+    std::vector<uint64_t> v(L->slots, 0);
+    for (uint32_t i = 0; i < L->slots; i++)
+        if (m[i] != kNoSlot && m[i] < s.v.size()) v[i] = s.v[m[i]];
+    s.v.swap(v);
+    s.layout = L;
+}
+
 // ---- Engine ------------------------------------------------------------------------------
 Engine::~Engine() {
     if (comm) dev_comm_destroy(comm);
@@ -243,24 +296,48 @@ int Engine::sync() {
         last_error = "upload: " + err;
         return PG_EIO;
     }
-    if (cur) dev_free(cur);  // waits for the launches that read the old set
+    // waits for the launches that read the old set -- among them every launch that counted into
+    // `counters` (pg_classify, pg_reset_counters record their use of it), so they are final
+    if (cur) dev_free(cur);
     cur = nb;
-    size_t slots = dev_view(cur).n_slots;
-    if (slots != counter_slots) {
-        if (counters) dev_release(counters);
-        counters = (unsigned long long*)dev_alloc(slots * sizeof(unsigned long long), &err);
-        if (!counters) {
-            last_error = err;
-            counter_slots = 0;
-            return PG_ENOMEM;
+    const size_t slots = dev_view(cur).n_slots;
+    // the counts of unchanged ACLs carry over to their new slots (slot_remap); changed and new
+    // ones start at zero. The device counters keep their address while the slot count holds.
+    const bool carry = counters && counted_layout;  // (else: nothing counted yet, or a failed sync)
+    bool identity = false;
+    std::vector<uint32_t> map;
+    if (carry) map = slot_remap(*counted_layout, *layout, &identity);
+    counted_layout = nullptr;  // until the counters are in the new layout
+    if (!(carry && identity)) {
+        unsigned long long* from = nullptr;  // the counts to carry: the old buffer or a copy of it
+        if (carry && slots == counter_slots) {  // remap through a copy, into the same buffer
+            from = (unsigned long long*)dev_alloc(counter_slots * 8, &err);
+            if (!from || dev_copy_d2d_async(from, counters, counter_slots * 8, nullptr, &err) != 0) {
+                dev_release(from);
+                last_error = err;
+                return PG_ENOMEM;
+            }
+        } else if (slots != counter_slots || !counters) {
+            unsigned long long* nc = (unsigned long long*)dev_alloc(slots * sizeof(unsigned long long), &err);
+            if (!nc) {
+                last_error = err;
+                return PG_ENOMEM;
+            }
+            if (carry) from = counters;
+            else dev_release(counters);
+            counters = nc;
+            counter_slots = slots;
         }
-        counter_slots = slots;
+        int rc = from ? dev_counters_remap(counters, from, map.data(), slots, &err)
+                      : dev_memset(counters, 0, slots * 8, nullptr, &err);
+        if (rc == 0) rc = dev_stream_sync(nullptr, &err);
+        dev_release(from);
+        if (rc != 0) {
+            last_error = err;
+            return PG_EIO;
+        }
     }
-    // slot meanings change with the tables: counters restart from zero
-    if (dev_memset(counters, 0, slots * 8, nullptr, &err) != 0 || dev_stream_sync(nullptr, &err) != 0) {
-        last_error = err;
-        return PG_EIO;
-    }
+    counted_layout = layout;
     dirty = false;
     return PG_OK;
 }
@@ -345,12 +422,20 @@ void Engine::compile() {
         auto L = std::make_shared<SlotLayout>();
         L->gen = ++layout_gen;
         for (uint32_t t = 0; t < T; t++)
-            L->tabs[table_names[t]] = SlotLayout::Tab{h.tabs[t].rule_base, h.tabs[t].n_rules, NR + t};
+            L->tabs[table_names[t]] = SlotLayout::Tab{h.tabs[t].rule_base, h.tabs[t].n_rules, NR + t,
+                                                      acl_rules_hash(*by_name.at(table_names[t]))};
         L->noacl = NR + T;
         L->unresolved = NR + T + 1;
         L->slots = NR + T + 2;
         layout = std::move(L);
+        // the host snapshots follow (the device counters follow at the upload, sync()): a gauge
+        // keyed by (ACL name, rule index) reads the same count before and after a recompile that
+        // left its ACL unchanged
+        std::lock_guard<std::mutex> lk(snap_mu);
+        remap_snapshot(snap_local, layout);
+        remap_snapshot(snap_cluster, layout);
     }
+    layout_gen_pub.store(layout_gen, std::memory_order_release);
 
     // interfaces
     iface_index.clear();

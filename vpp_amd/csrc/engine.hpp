@@ -3,6 +3,7 @@
 // 655-712), compiles them into the device table set (device.hpp) and evaluates
 // evalACL/testConnection on the GPU.
 #pragma once
+#include <atomic>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -27,10 +28,22 @@ struct SlotLayout {
     uint64_t gen = 0;  // Engine::layout_gen when compiled
     struct Tab {
         uint32_t base, n, dflt;
+        uint64_t rules_hash;  // FNV-64a over the ACL's rules (acl_rules_hash)
     };
     std::map<std::string, Tab> tabs;  // ACL name -> its slots
     uint32_t noacl = 0, unresolved = 0, slots = 0;
 };
+
+// FNV-64a over every field of an ACL's rules, in order (the identity its counts carry over by)
+uint64_t acl_rules_hash(const ACL& acl);
+
+// Counts that survive a recompile (statscollector: a gauge is a monotonic source,
+// plugin_impl_statscollector.go:248-261): map[new slot] = the slot of `from` whose count it
+// continues, or kNoSlot (starts at zero). An ACL carries over when an ACL of the same name with
+// the same rules (count and acl_rules_hash) exists in both layouts -- its rule slots and its
+// default-deny slot; "no ACL" and "unresolved" always do. Identity: every slot maps to itself.
+constexpr uint32_t kNoSlot = 0xFFFFFFFFu;
+std::vector<uint32_t> slot_remap(const SlotLayout& from, const SlotLayout& to, bool* identity = nullptr);
 
 // A host copy of the counters and the layout they were counted in.
 struct CounterSnapshot {
@@ -78,8 +91,13 @@ struct Engine {
     unsigned long long* reduced = nullptr;
     size_t reduced_slots = 0;
     // slot layout of the compiled set; layout_gen counts the recompiles that renumbered slots
+    // (published for pg_counter_layout_gen, which any thread may poll, through layout_gen_pub)
     std::shared_ptr<const SlotLayout> layout;
     uint64_t layout_gen = 0;
+    std::atomic<uint64_t> layout_gen_pub{0};
+    // the layout of the uploaded set, which the device counters are counted in: sync() carries
+    // them over (slot_remap) to the next set's layout
+    std::shared_ptr<const SlotLayout> counted_layout;
     // host copies of the counters, read by the statscollector gauges without touching the GPU
     // (pg_counters_snapshot*): this rank's own as of the last pg_read_counters, and the sum over
     // the communicator as of the last pg_allreduce_counters*. Gauges run on their own threads

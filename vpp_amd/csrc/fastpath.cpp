@@ -726,13 +726,15 @@ void node_point_leaves(std::vector<uint32_t>& b, uint32_t root, uint32_t s1, boo
 // ---- FD blob: the fixed-depth form of a dst-independent CROSS table --------------------------
 // Layout (u32 words; trie entries hold WORD offsets, kEncWords, so a blob is < 16 MiB):
 //   [0] kFlagFD  [1] default verdict  [2] src root (16)  [3] s1  [4] key root  [5] k1
-//   [6] depth D (reads per field, root included)  [7] bias = 1 - KSELF  [8] n_key_classes
+//   [6] depths (reads per field, root included): src trie in bits 0-7, key trie in bits 8-15
+//       (equal when both walks run in lockstep; blobwalk.hpp fd_walk)  [7] bias = 1 - KSELF
+//   [8] n_key_classes
 //   [9] stage words (the prefix below)  [10] n_src_classes
 //   prefix: header | src root block | key trie (all levels) | KSELF: one self word per key class
 //   then:   src trie levels below the root | rows: per src class c {self word, verdict[c][0..nkc-1]}
 // A self word at word A holds A << 10 (stride 0: reading "its child" reads itself). Trie leaves
 // point at self words: src -> its class's row head, key -> its class's self word. Every lookup
-// is exactly D reads per field plus one verdict read at
+// is exactly its field's depth in reads plus one verdict read at
 //   (src self) + 1 + key class = (src self) + (key self) + bias,
 // with no per-lane branch (fd_walk). The prefix -- everything a key lookup and the src root
 // read touch -- is what a launch stages in LDS when the whole blob does not fit (device.hip
@@ -1257,6 +1259,14 @@ bool build_node(HostTableSet& h, const std::vector<TableAnalysis*>& an, const st
         N.img_words = (uint32_t)img.size();
     }
     if (X.empty()) X.resize(4, 0);
+    if (std::getenv("PG_NODE_DEBUG"))  // measurement aid: the image's shape
+        std::fprintf(stderr,
+                     "node: T %u G %u GK %u uniform %u | ip root %u depth %u, key root %u depth %u | words: "
+                     "ip trie %u, key trie %u, ip rec %u, key rec %u, tabinfo+kmap %u, common %u, lists %u, total %u\n",
+                     T, N.n_ipc, N.gk, N.uniform, N.ip_s1, N.ip_depth, N.key_k1, N.key_depth, N.key_root,
+                     irec0 - N.key_root, krec0 - irec0, N.tabinfo - krec0, N.img_words_base - N.tabinfo,
+                     (N.lrec ? N.lrec : N.img_words) - N.img_words_base, N.lrec ? N.img_words - N.lrec : 0,
+                     N.img_words);
     return true;
 }
 
