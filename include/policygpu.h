@@ -168,8 +168,11 @@ int pg_ctx_device(const pg_ctx* ctx);
  * no live rule of which tests dst, default 1), "fd" (1/0: fixed-depth form of dst-independent
  * cross-product tables, default 1), "node_common" (1/0: common-row section of node
  * images, default 1), "node_uniform" (1/0: the node's uniform cross layout where every table
- * is covered and none is in PAIR form, default 1), "node_list_words" (node dst records -- the dst-specific rules a node
- * cross entry must still test -- up to this many words go into the node image, so a launch that
+ * is covered and none is in PAIR form, default 1), "node_list_table" (1/0: a node cross entry
+ * whose table still has dst-specific rules ahead of its verdict resolves them by one read of a
+ * list-verdict table indexed by the dst's node IP class -- the IPv4 classes then also separate
+ * those rules' dst prefixes -- instead of walking dst records; default 1), "node_list_words"
+ * (record form: node dst records up to this many words go into the node image, so a launch that
  * stages the image walks them in LDS; default 4096, 0 = never), "pair" (1/0: the PAIR structure -- src x dst classes, then x key classes
  * -- for tables the cross product cannot take, default 1; 0 = candidate lists; 2 = wherever it
  * fits, for tests).
@@ -251,9 +254,9 @@ int pg_debug_classify_host(pg_ctx* ctx, int mode, int table_id, const pg_tuple_s
  * pg_debug_classify_host) as the LOCAL or CLUSTER snapshot in the currently compiled slot layout,
  * so the snapshot readers below can be tested without a GPU. n must equal the slot count. */
 int pg_debug_set_snapshot(pg_ctx* ctx, int which, const uint64_t* counters, size_t n);
-/* TESTS ONLY -- never on the classify path: the per-stream launch-mark bookkeeping of CONN launches
+/* TESTS ONLY -- never on the classify path: the per-stream launch-mark bookkeeping of PERPOD / CONN launches
  * (device.hpp StreamSlots, which pg_classify uses to hand a launch's deferred ANY-protocol packets
- * to the k_conn_any launched after it on the same stream) replayed for n launches on the given
+ * to the k_node_any launched after it on the same stream) replayed for n launches on the given
  * stream handles: slot_out[k] = the mark word launch k writes, seq_out[k] = its launch number. No
  * device work. */
 int pg_debug_stream_slots(const uint64_t* streams, size_t n, uint32_t* slot_out, uint32_t* seq_out);
@@ -273,9 +276,13 @@ int pg_node_stats(pg_ctx* ctx, uint32_t* ip_classes, uint32_t* key_classes, uint
  * the covered (table, IPv4 class) pairs read the table's common row from the image instead of
  * the cross table (0 when the section was not built); PG_ENOENT when there is no node */
 int pg_node_common_stats(pg_ctx* ctx, uint64_t* base_image_bytes, uint64_t* common_pairs, uint64_t* pairs);
-/* the node classifier's dst records (the dst-specific rules its cross entries still test): their
- * bytes, and whether a copy ends the node image (tuning "node_list_words"); PG_ENOENT: no node */
+/* the node classifier's dst records (the dst-specific rules its cross entries still test, record
+ * form): their bytes, and whether a copy ends the node image (tuning "node_list_words"); 0 bytes in
+ * the list-table form (pg_node_list_table_stats); PG_ENOENT: no node */
 int pg_node_list_stats(pg_ctx* ctx, uint64_t* record_bytes, int* in_image);
+/* the node classifier's list-verdict table (tuning "node_list_table"): its bytes in the cross
+ * array (0 = the record form, or no lists); PG_ENOENT: no node */
+int pg_node_list_table_stats(pg_ctx* ctx, uint64_t* table_bytes);
 /* 1 when the node classifier uses the uniform cross layout (every table covered, none in PAIR
  * form, tuning "node_uniform": entry addresses computed, no per-table info reads), else 0;
  * PG_ENOENT: no node */

@@ -439,9 +439,10 @@ def test_node_kernel_equals_per_table_kernel(config):
 @pytest.mark.parametrize("config", [3, 5])
 def test_node_launch_variants(config):
     """Every node launch shape, with and without counters, equals the default launch and the
-    host run: the image with its common rows but without the dst records (records from the
-    cross array), and a build without common rows (records staged right after the base image,
-    or left in the cross array)."""
+    host run. List-verdict table form (default): with and without the common-row section. Record
+    form (node_list_table=0): the image with its common rows but without the dst records
+    (records from the cross array), and a build without common rows (records staged right after
+    the base image, or left in the cross array)."""
     from vpp_amd import workloads as W
     w = W.CONFIGS[config](0, n_tuples=(1 << 19) + 5)
     e = w.engine
@@ -452,24 +453,34 @@ def test_node_launch_variants(config):
     assert np.array_equal(ref, ref0)
     assert np.array_equal(e.debug_classify_host(w.mode, -1, *b.numpy(b.n), node=True), ref)
     ns = e.node_stats()
-    assert ns["list_records_in_image"] and ns["list_record_bytes"] and ns["common_row_pairs"]
-    norec = ns["image_bytes"] - ns["list_record_bytes"]
+    assert ns["list_table_bytes"] and not ns["list_record_bytes"] and ns["common_row_pairs"]
     hist = (e.num_counter_slots() + 2) * 4
-    for counters in (True, False):
-        h = hist if counters else 0
-        # the common rows staged, the records not (lrec cleared: read from the cross array)
-        got, c = _classify_with(e, w.mode, b, 1, counters=counters, common_lds=h + norec + 16)
-        assert np.array_equal(got, ref) and (not counters or np.array_equal(c, cref))
-    with e.tuning(node_common=0):
-        ns2 = e.node_stats()
-        assert ns2["common_row_pairs"] == 0 and ns2["list_records_in_image"]
-        base = ns2["base_image_bytes"] // 4
+    with e.tuning(node_common=0):  # the table form without common rows (STAGE 1)
+        assert e.node_stats()["common_row_pairs"] == 0
         for counters in (True, False):
-            got, c = _classify_with(e, w.mode, b, 1, counters=counters)  # STAGE 1, records staged
+            got, c = _classify_with(e, w.mode, b, 1, counters=counters)
             assert np.array_equal(got, ref) and (not counters or np.array_equal(c, cref))
-            # STAGE 1 with the base image only: records from the cross array
-            got, c = _classify_with(e, w.mode, b, 1, stage_words=base, counters=counters)
+    with e.tuning(node_list_table=0):
+        ns = e.node_stats()
+        assert ns["list_records_in_image"] and ns["list_record_bytes"] and ns["common_row_pairs"]
+        norec = ns["image_bytes"] - ns["list_record_bytes"]
+        for counters in (True, False):
+            h = hist if counters else 0
+            got, c = _classify_with(e, w.mode, b, 1, counters=counters)  # everything staged
             assert np.array_equal(got, ref) and (not counters or np.array_equal(c, cref))
+            # the common rows staged, the records not (lrec cleared: read from the cross array)
+            got, c = _classify_with(e, w.mode, b, 1, counters=counters, common_lds=h + norec + 16)
+            assert np.array_equal(got, ref) and (not counters or np.array_equal(c, cref))
+        with e.tuning(node_common=0):
+            ns2 = e.node_stats()
+            assert ns2["common_row_pairs"] == 0 and ns2["list_records_in_image"]
+            base = ns2["base_image_bytes"] // 4
+            for counters in (True, False):
+                got, c = _classify_with(e, w.mode, b, 1, counters=counters)  # STAGE 1, records staged
+                assert np.array_equal(got, ref) and (not counters or np.array_equal(c, cref))
+                # STAGE 1 with the base image only: records from the cross array
+                got, c = _classify_with(e, w.mode, b, 1, stage_words=base, counters=counters)
+                assert np.array_equal(got, ref) and (not counters or np.array_equal(c, cref))
 
 
 def test_large_table_root_staged_and_hbm_walks_equal_oracle():

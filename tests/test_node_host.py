@@ -179,33 +179,45 @@ def test_config3_cluster_node_path():
     assert np.array_equal(got >> 30, conn.astype(np.uint32)) and np.array_equal(got & 0x3FFFFFFF, cslot)
     got0 = e.debug_classify_host(MODE_CONN, -1, src, dst, sport, dport, proto, node=True, common=False)
     assert np.array_equal(got0, got)
-    # the global table's dst-specific rules: dst records, a copy at the end of the image
-    assert ns["list_record_bytes"] > 0 and ns["list_records_in_image"], ns
+    # the global table's dst-specific rules: resolved by the list-verdict table (no records)
+    assert ns["list_table_bytes"] > 0 and ns["list_record_bytes"] == 0, ns
     # every table covered, none in PAIR form: the uniform cross layout
     assert ns["uniform"], ns
 
 
-def test_node_dst_records_in_image_or_cross():
-    """Node dst records read from the image copy (default) and from the cross array
-    (node_list_words=0: no copy) classify the same, and equal the oracle."""
+def test_node_lists_table_or_records_in_image_or_cross():
+    """A node cross entry with dst-specific rules ahead of its verdict resolves them the same
+    three ways, all equal to the oracle: by the list-verdict table (default: one read at [list]
+    [dst's node IP class]), by dst records copied into the image (node_list_table=0), and by
+    records read from the cross array (node_list_table=0, node_list_words=0: no copy)."""
     w = W.config3(0, n_tuples=1 << 10, n_ns=4)
     src, dst, sport, dport, proto = gen.gen_tuples(30001, **w.gen)
     ns = w.engine.node_stats()
-    assert ns["list_records_in_image"] and ns["image_bytes"] >= ns["list_record_bytes"], ns
+    assert ns["list_table_bytes"] > 0 and ns["list_record_bytes"] == 0 and not ns["list_records_in_image"], ns
     a = w.engine.debug_classify_host(MODE_PERPOD, -1, src, dst, sport, dport, proto, node=True)
     c = w.engine.debug_classify_host(MODE_CONN, -1, src, dst, sport, dport, proto, node=True)
-    assert _capi.lib.pg_set_tuning(b"node_list_words", 0) == 0
+    assert _capi.lib.pg_set_tuning(b"node_list_table", 0) == 0
     try:
+        w1 = W.config3(0, n_tuples=1 << 10, n_ns=4)
+        ns1 = w1.engine.node_stats()
+        assert ns1["list_records_in_image"] and ns1["list_table_bytes"] == 0, ns1
+        assert ns1["image_bytes"] >= ns1["list_record_bytes"] > 0, ns1
+        assert np.array_equal(w1.engine.debug_classify_host(MODE_PERPOD, -1, src, dst, sport, dport, proto, node=True), a)
+        assert np.array_equal(w1.engine.debug_classify_host(MODE_CONN, -1, src, dst, sport, dport, proto, node=True), c)
+        assert _capi.lib.pg_set_tuning(b"node_list_words", 0) == 0
         w2 = W.config3(0, n_tuples=1 << 10, n_ns=4)
         ns2 = w2.engine.node_stats()
-        assert not ns2["list_records_in_image"] and ns2["image_bytes"] == ns["image_bytes"] - ns["list_record_bytes"]
+        assert not ns2["list_records_in_image"] and ns2["image_bytes"] == ns1["image_bytes"] - ns1["list_record_bytes"]
         assert np.array_equal(w2.engine.debug_classify_host(MODE_PERPOD, -1, src, dst, sport, dport, proto, node=True), a)
         assert np.array_equal(w2.engine.debug_classify_host(MODE_CONN, -1, src, dst, sport, dport, proto, node=True), c)
     finally:
         assert _capi.lib.pg_set_tuning(b"node_list_words", 4096) == 0
+        assert _capi.lib.pg_set_tuning(b"node_list_table", 1) == 0
     wd = World(w.engine, w.local_ifs, w.node_if)
     act, slot = wd.perpod(src, dst, dport, proto, threads=8)
     assert np.array_equal(a >> 30, act.astype(np.uint32)) and np.array_equal(a & 0x3FFFFFFF, slot)
+    conn, cslot = wd.conn(src, dst, sport, dport, proto, threads=8)
+    assert np.array_equal(c >> 30, conn.astype(np.uint32)) and np.array_equal(c & 0x3FFFFFFF, cslot)
 
 
 def test_common_rows_disabled():

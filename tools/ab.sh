@@ -5,6 +5,8 @@
 #   gpurun -- bash tools/ab.sh TAG "libA libB" "3 5c 6" [pytest paths]
 # PRE="key=v ..." (environment): compiler knobs set before the tables are built (sweep.py --pre)
 # TUNE="key=v1,v2 ..." (environment): launch knobs swept inside each run (sweep.py --tune)
+# SWEEP="..." (environment): the sweep's own arguments (default --rounds 3 --reps 5 after 60
+#   warm-up launches); SWEEP="--warmup 5 --rounds 1 --reps 20" times the driver's window
 set -o pipefail
 TAG=${1:-ablib}; LIBS=${2:-libpolicygpu.so}; CONFIGS=${3:-3}; TESTS=${4:-}
 R=$(pwd)
@@ -17,7 +19,7 @@ if [ -n "$TESTS" ]; then
         > "$O/gpu_tests.log" 2>&1 || { tail -30 "$O/gpu_tests.log"; exit 1; }
     tail -2 "$O/gpu_tests.log"
 fi
-for r in 1 2; do
+for r in $(seq ${ROUNDS:-2}); do
 for lib in $LIBS; do
     for c in $CONFIGS; do
         cnt=""; case $c in *c) cnt="--counters";; esac
@@ -25,7 +27,7 @@ for lib in $LIBS; do
         step sweep $lib config $c $cnt $extra
         pre=""; for kv in ${PRE:-}; do pre="$pre --pre $kv"; done
         for kv in ${TUNE:-}; do pre="$pre --tune $kv"; done
-        VPP_AMD_LIB=$R/vpp_amd/$lib timeout -k 10 200 python tools/sweep.py --config ${c%c} --rounds 3 --reps 5 $cnt $pre $extra \
+        VPP_AMD_LIB=$R/vpp_amd/$lib timeout -k 10 200 python tools/sweep.py --config ${c%c} ${SWEEP:---rounds 3 --reps 5} $cnt $pre $extra \
             >> "$O/sweep.jsonl" 2> "$O/sweep.err" || { tail -20 "$O/sweep.err"; exit 1; }
     done
 done

@@ -169,6 +169,7 @@ _SIGS = {
                                 C.POINTER(C.c_uint64)]),
     "pg_node_common_stats": (C.c_int, [_P, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
     "pg_node_list_stats": (C.c_int, [_P, C.POINTER(C.c_uint64), C.POINTER(C.c_int)]),
+    "pg_node_list_table_stats": (C.c_int, [_P, C.POINTER(C.c_uint64)]),
     "pg_node_uniform": (C.c_int, [_P]),
     "pg_configurator_new": (_P, []),
     "pg_configurator_free": (None, [_P]),
@@ -241,11 +242,15 @@ _SIGS = {
 EXPORTED = sorted(_SIGS)
 
 
-def load(path=LIB_PATH):
+def load(path=LIB_PATH, partial=False):
+    """partial: an A/B build of an earlier revision (tools/sweep.py) may lack entry points added
+    since; they are left unbound instead of failing the load"""
     if not os.path.exists(path):
         raise ImportError("libpolicygpu.so not built (%s): run __graft_entry__.build()" % path)
     lib = C.CDLL(path)
     for name, (res, args) in _SIGS.items():
+        if partial and not hasattr(lib, name):
+            continue
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
@@ -253,4 +258,4 @@ def load(path=LIB_PATH):
 
 
 # VPP_AMD_LIB: load an A/B build of the same library (tools/sweep.py); default the in-tree build
-lib = load(os.environ.get("VPP_AMD_LIB", LIB_PATH))
+lib = load(os.environ.get("VPP_AMD_LIB", LIB_PATH), partial="VPP_AMD_LIB" in os.environ)

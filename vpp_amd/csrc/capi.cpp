@@ -785,6 +785,18 @@ int pg_node_list_stats(pg_ctx* ctx, uint64_t* record_bytes, int* in_image) {
     GUARD_END(ctx)
 }
 
+int pg_node_list_table_stats(pg_ctx* ctx, uint64_t* table_bytes) {
+    if (!ctx) return PG_EINVAL;
+    GUARD_BEGIN
+    Engine& E = ctx->eng;
+    if (!E.compiled) E.compile();
+    const HostTableSet& h = E.host;
+    if (h.node_img.empty()) return fail(ctx, PG_ENOENT, "no node classifier (disabled or over budget)");
+    if (table_bytes) *table_bytes = (uint64_t)h.node_list_tab_words * 4;
+    return PG_OK;
+    GUARD_END(ctx)
+}
+
 int pg_node_uniform(pg_ctx* ctx) {
     if (!ctx) return PG_EINVAL;
     GUARD_BEGIN
@@ -811,8 +823,8 @@ int pg_classify(pg_ctx* ctx, int mode, int table_id, const pg_tuple_soa* t, uint
         return fail(ctx, PG_EINVAL, "missing tuple field");
     std::string err;
     DevTableSet TL = T;
-    // CONN: the launch stream's mark word and this launch's number (device.hpp StreamSlots)
-    if (mode == PG_MODE_CONN && !(TL.any_mark = dev_any_mark(ctx->eng.cur, stream, &TL.any_seq, &err)))
+    // PERPOD / CONN: the launch stream's mark word and this launch's number (device.hpp StreamSlots)
+    if (mode != PG_MODE_SINGLE && !(TL.any_mark = dev_any_mark(ctx->eng.cur, stream, &TL.any_seq, &err)))
         return fail(ctx, PG_EIO, err);
     if (dev_classify(TL, ctx->eng.tune, mode, table_id, t->src_ip, t->dst_ip, t->src_port, t->dst_port, t->proto, n,
                      out, (unsigned long long*)counters, stream, &err) != 0 ||

@@ -56,6 +56,22 @@ PG_HD uint32_t mul24(uint32_t a, uint32_t b) {
     return a * b;
 #endif
 }
+// a * b + c for a, b below 2^24 (v_mad_u32_u24 on the device)
+PG_HD uint32_t mad24(uint32_t a, uint32_t b, uint32_t c) {
+#if defined(__HIP_DEVICE_COMPILE__) && PG_MUL24
+    return __umul24(a, b) + c;
+#else
+    return a * b + c;
+#endif
+}
+// bit i & 31 of w (one v_bfe_u32: its offset operand reads the low 5 bits)
+PG_HD uint32_t bit_of(uint32_t w, uint32_t i) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_ubfe(w, i, 1u);
+#else
+    return (w >> (i & 31u)) & 1u;
+#endif
+}
 constexpr uint32_t kSlotMask = 0x3FFFFFFFu;
 
 PG_HD uint32_t hash_ip(uint32_t ip) {
@@ -568,33 +584,43 @@ PG_HD void node_trie_q(const L& ld, uint32_t root, uint32_t s1, uint32_t W, uint
 
 // The IPv4 trie (addresses a) and the L4-key trie (keys b) in one lockstep loop: independent
 // walks, so their dependent LDS reads overlap. rr: the IPv4 class records' byte addresses; cb:
-// the key classes.
-template <bool PRED, bool A, class L, int QA, int QB>
+// the key classes. IS1 / ID / KS1 / KD: the tries' root strides and depths when known at compile
+// time (node_walks: the common shapes), so every level's shift is a constant and the walks
+// unroll into straight-line code; 0 = read from N at run time.
+template <bool PRED, bool A, uint32_t IS1 = 0, uint32_t ID = 0, uint32_t KS1 = 0, uint32_t KD = 0, class L, int QA,
+          int QB>
 PG_HD void node_trie2_q(const L& ld, const DevNode& N, const uint32_t (&a)[QA], uint32_t (&rr)[QA],
                         const uint32_t (&b)[QB], uint32_t (&cb)[QB]) {
-    uint32_t ea[QA], eb[QB], ra = 32u - N.ip_s1, rb = 18u - N.key_k1;
+    const uint32_t is1 = IS1 ? IS1 : N.ip_s1, ks1 = KS1 ? KS1 : N.key_k1;
+    const uint32_t idp = ID ? ID : N.ip_depth, kdp = KD ? KD : N.key_depth;
+    uint32_t ea[QA], eb[QB], ra = 32u - is1, rb = 18u - ks1;
     PG_UNROLL
-    for (int j = 0; j < QA; j++) ea[j] = ld.u32(a[j] >> (32u - N.ip_s1));
+    for (int j = 0; j < QA; j++) ea[j] = ld.u32(a[j] >> (32u - is1));
     PG_UNROLL
-    for (int j = 0; j < QB; j++) eb[j] = ld.u32(N.key_root + (b[j] >> (18u - N.key_k1)));
-    const uint32_t dmin = N.ip_depth < N.key_depth ? N.ip_depth : N.key_depth;
-    for (uint32_t l = 1; l < dmin; l++) {
-        ra = node_next_shift(ra);
-        rb = node_next_shift(rb);
-        PG_UNROLL
-        for (int j = 0; j < QA; j++) ea[j] = ld.at_byte(node_child_byte<A>(ea[j], a[j], ra));
-        PG_UNROLL
-        for (int j = 0; j < QB; j++) eb[j] = ld.at_byte(node_child_byte<A>(eb[j], b[j], rb));
-    }
-    for (uint32_t l = dmin; l < N.ip_depth; l++) {
+    for (int j = 0; j < QB; j++) eb[j] = ld.u32(N.key_root + (b[j] >> (18u - ks1)));
+    const uint32_t dmin = idp < kdp ? idp : kdp;
+    auto step_a = [&]() {
         ra = node_next_shift(ra);
         PG_UNROLL
         for (int j = 0; j < QA; j++) ea[j] = ld.at_byte(node_child_byte<A>(ea[j], a[j], ra));
-    }
-    for (uint32_t l = dmin; l < N.key_depth; l++) {
+    };
+    auto step_b = [&]() {
         rb = node_next_shift(rb);
         PG_UNROLL
         for (int j = 0; j < QB; j++) eb[j] = ld.at_byte(node_child_byte<A>(eb[j], b[j], rb));
+    };
+    if constexpr (ID != 0 && KD != 0) {  // straight-line code, constant shifts
+        constexpr uint32_t DM = ID < KD ? ID : KD;
+        PG_UNROLL
+        for (uint32_t l = 1; l < DM; l++) step_a(), step_b();
+        PG_UNROLL
+        for (uint32_t l = DM; l < ID; l++) step_a();
+        PG_UNROLL
+        for (uint32_t l = DM; l < KD; l++) step_b();
+    } else {
+        for (uint32_t l = 1; l < dmin; l++) step_a(), step_b();
+        for (uint32_t l = dmin; l < idp; l++) step_a();
+        for (uint32_t l = dmin; l < kdp; l++) step_b();
     }
     PG_UNROLL
     for (int j = 0; j < QA; j++) rr[j] = A ? ea[j] : ea[j] >> 5;
@@ -605,6 +631,26 @@ PG_HD void node_trie2_q(const L& ld, const DevNode& N, const uint32_t (&a)[QA], 
 #ifndef PG_NODE_WALK2  // node kernels: IPv4 and key tries in one lockstep walk
 #define PG_NODE_WALK2 1
 #endif
+#ifndef PG_NODE_SHAPES  // uniform-layout walks: the common trie shapes compiled with constant shifts
+#define PG_NODE_SHAPES 1
+#endif
+
+// node_trie2_q, with the tries' shape as compile-time constants when it is one of the common ones
+// of the uniform layout (aligned tries: IPv4 root 8 bits + three 8-bit levels; key root 6 bits +
+// 8 + 4, or 2 bits + 8 + 8 -- fastpath.cpp build_node picks the fewest levels, then the smallest
+// image), else read at run time. The shape test is uniform (a scalar branch).
+template <bool PRED, bool A, class L, int QA, int QB>
+PG_HD void node_walks(const L& ld, const DevNode& N, const uint32_t (&a)[QA], uint32_t (&rr)[QA],
+                      const uint32_t (&b)[QB], uint32_t (&cb)[QB]) {
+    if constexpr (A && PG_NODE_SHAPES) {
+        const uint32_t shape = N.ip_s1 | N.ip_depth << 8 | N.key_k1 << 16 | N.key_depth << 24;
+        if (shape == (8u | 4u << 8 | 6u << 16 | 3u << 24))
+            return node_trie2_q<PRED, A, 8, 4, 6, 3>(ld, N, a, rr, b, cb);
+        if (shape == (8u | 4u << 8 | 2u << 16 | 3u << 24))
+            return node_trie2_q<PRED, A, 8, 4, 2, 3>(ld, N, a, rr, b, cb);
+    }
+    node_trie2_q<PRED, A>(ld, N, a, rr, b, cb);
+}
 
 // end point of a node IP class outside the uniform layout (ipinfo: {interface, tin | tout << 16},
 // 0xFFFF = no ACL); the uniform layout's class records pack it (node_end_packed)
@@ -677,11 +723,15 @@ struct NodeEval {
                 uint32_t cw = 0;
                 if (CM) {  // bit t of the rule-src-side class's mask
                     const W2 m = rev ? (*msk_d)[j] : (*msk_s)[j];
-                    cw = (tt < 32u ? m.x : m.y) >> (tt & 31u);
+                    cw = bit_of(tt < 32u ? m.x : m.y, tt);
                 }
                 on[j] = act[j] && k[j] < kWalkKeyLimit;
-                cm[j] = CM && (cw & 1u);
-                pos[j] = cm[j] ? N.crow0 + mul24(tt, N.gk) + gk[j] : mul24(mul24(tt, N.n_ipc) + ca[j], N.gk) + gk[j];
+                cm[j] = CM && cw != 0u;
+                // both addresses, then a select (no branch): the common row's entry in the image,
+                // or the cross entry (t * G + class) * GK + key class = t * tstride + class * GK + k
+                const uint32_t pc = mad24(tt, N.gk, N.crow0 + gk[j]);
+                const uint32_t px = mad24(tt, N.tstride, mad24(ca[j], N.gk, gk[j]));
+                pos[j] = cm[j] ? pc : px;
                 fb[j] = act[j] && !on[j];
                 pr[j] = false;
             }
@@ -760,8 +810,18 @@ struct NodeEval {
             pend[j] = (w[j] & kNodeList) != 0u;
             pos[j] = (w[j] & kNodeRecMask) << 2;
         }
-        // dst records until the first match (every list ends with a match-all record): from the
-        // image (N.lrec, uniform) or the cross array
+        // list-verdict table (N.lv0): one read at [list][node IP class of the rule's dst-side
+        // address] (fastpath.cpp build_node)
+        if (N.lv0) {
+            const uint32_t(&cb)[Q] = rev ? cs : cd;
+            PG_UNROLL
+            for (int j = 0; j < Q; j++)
+                if (pend[j]) w[j] = X.u32(N.lv0 + (w[j] & kNodeRecMask) * N.n_ipc + cb[j]);
+            PG_UNROLL
+            for (int j = 0; j < Q; j++) pend[j] = false;
+        }
+        // record form: dst records until the first match (every list ends with a match-all
+        // record), from the image (N.lrec, uniform) or the cross array
         auto walk = [&](const auto& R, uint32_t delta) {
             for (;;) {
                 bool more = false;
@@ -967,6 +1027,22 @@ PG_HD uint32_t conn_any_1(const DevTableSet& T, uint32_t s, uint32_t d, const HS
     return o[0];
 }
 
+// the per-pod evaluation (the outbound ACL of dst's interface) of one ANY-protocol packet through
+// the iphash and AnyEval (the PERPOD node build's deferred pass, device.hip PG_POD_DEFER_ANY)
+template <bool COUNT, class HS>
+PG_HD uint32_t pod_any_1(const DevTableSet& T, uint32_t s, uint32_t d, const HS& h) {
+    const uint32_t d1[1] = {d}, s1[1] = {s};
+    End e[1];
+    probe_q(T, d1, e);
+    const bool run[1] = {e[0].ifc >= 0};
+    const int32_t t[1] = {e[0].tout};
+    uint32_t o[1] = {verdict(kActFailure, T.slot_unresolved)};
+    if (COUNT && !run[0]) h.inc_cold(T.slot_unresolved);
+    const AnyEval<1> ev{T, s1, d1};
+    eval_step<1, COUNT>(T, ev, t, run, false, h, o);
+    return o[0];
+}
+
 // Q tuples of one lane, any mode, per-table path. SINGLE: tab0 is the (uniform) table, its
 // blob at `blobs`.
 template <int MODE, bool COUNT, int Q, bool PRED = false, class HS = Hist>
@@ -1019,9 +1095,10 @@ PG_HD void classify_q(const DevTableSet& T, const uint32_t* blobs, const DevTabl
 
 // Q tuples of one lane, PERPOD / CONN, node path. `img` reads the node image (LDS copy or
 // global memory).
-// DEFER (CONN over a uniform node, every table covered): ANY-protocol packets (the only ones
-// the node cannot classify) are left to the caller -- no evaluation, no count, a placeholder
-// verdict -- so the evaluation carries no per-table fallback (device.hip PG_CONN_DEFER_ANY)
+// DEFER (PERPOD / CONN over a uniform node, every table covered): ANY-protocol packets (the
+// only ones the node cannot classify) are left to the caller -- no evaluation, no count, a
+// placeholder verdict -- so the evaluation carries no per-table fallback (device.hip
+// PG_CONN_DEFER_ANY, PG_POD_DEFER_ANY)
 template <int MODE, bool COUNT, int Q, bool PRED = false, bool CM = false, bool NP = false, bool UNI = false,
           bool DEFER = false, class L, class HS, class H = NoHook>
 PG_HD void classify_node_q(const DevTableSet& T, const DevNode& N, const L& img, const uint32_t (&s)[Q],
@@ -1043,7 +1120,7 @@ PG_HD void classify_node_q(const DevTableSet& T, const DevNode& N, const L& img,
             keys[j] = key[j] < kWalkKeyLimit ? key[j] : 0u;
             keys[Q + j] = kack[j] < kWalkKeyLimit ? kack[j] : 0u;
         }
-        node_trie2_q<PRED, UNI>(img, N, ips, rec, keys, kc);
+        node_walks<PRED, UNI>(img, N, ips, rec, keys, kc);
         PG_UNROLL
         for (int j = 0; j < Q; j++) gs[j] = kc[j], ga[j] = kc[Q + j];
     } else {
@@ -1055,12 +1132,12 @@ PG_HD void classify_node_q(const DevTableSet& T, const DevNode& N, const L& img,
             uint32_t sa[Q], sr[Q];
             PG_UNROLL
             for (int j = 0; j < Q; j++) sa[j] = ips[j];
-            node_trie2_q<PRED, UNI>(img, N, sa, sr, keys, gs);
+            node_walks<PRED, UNI>(img, N, sa, sr, keys, gs);
             PG_UNROLL
             for (int j = 0; j < Q; j++) rec[j] = sr[j], rec[Q + j] = sr[j];
         }
 #else
-        node_trie2_q<PRED, UNI>(img, N, ips, rec, keys, gs);
+        node_walks<PRED, UNI>(img, N, ips, rec, keys, gs);
 #endif
         PG_UNROLL
         for (int j = 0; j < Q; j++) ga[j] = gs[j];
@@ -1112,18 +1189,20 @@ PG_HD void classify_node_q(const DevTableSet& T, const DevNode& N, const L& img,
             ed[j] = node_end(img, N, cd[j]);
         }
     }
-    constexpr bool DF = DEFER && MODE == 2 && UNI;
+    constexpr bool DF = DEFER && UNI;
     const NodeEval<L, Q, H, CM, NP || UNI, UNI, DF> ev{T, N, img, s, d, key, kack, cs, cd, gs, ga, hook, &hooked, &mks, &mkd};
     if (MODE == 1) {
         int32_t t[Q];
         bool run[Q];
         PG_UNROLL
         for (int j = 0; j < Q; j++) {
-            run[j] = ed[j].ifc >= 0;
+            // (DF) an ANY-protocol packet: left to the caller (placeholder verdict, no count)
+            const bool df = DF && key[j] >= kWalkKeyLimit;
+            run[j] = !df && ed[j].ifc >= 0;
             t[j] = ed[j].tout;
             if (!run[j]) {
                 out[j] = verdict(kActFailure, T.slot_unresolved);
-                if (COUNT) h.inc_cold(T.slot_unresolved);
+                if (COUNT && !df) h.inc_cold(T.slot_unresolved);
             }
         }
         eval_step<Q, COUNT>(T, ev, t, run, false, h, out);

@@ -56,7 +56,7 @@ struct DeviceBuffers {
     };
     std::vector<Use> uses;  // uses[i]: the stream of slot i (StreamSlots)
     StreamSlots slots;
-    uint32_t* marks = nullptr;  // device: StreamSlots::kMax launch-mark words (CONN, k_conn_any)
+    uint32_t* marks = nullptr;  // device: StreamSlots::kMax launch-mark words (k_node_any)
 };
 
 const DevTableSet& dev_view(const DeviceBuffers* b) { return b->view; }
@@ -476,34 +476,44 @@ constexpr size_t kLdsPerCU = 160u << 10;
 #define PG_NODE_FULLH 1
 #endif
 // CONN over a uniform node (STAGE + 96): ANY-protocol packets, the only ones the node cannot
-// classify, are deferred to k_conn_any, launched after the classify kernel on the same stream
+// classify, are deferred to k_node_any, launched after the classify kernel on the same stream
 // (iphash end points, the ANY-protocol first match, global counter increments), so the
 // classify kernel carries no per-table fallback. The out-of-line fallback call in the loop
 // cost the kernel its SGPR allocation: 54 SGPRs spilled to VGPR lanes, a v_readlane per use;
 // a pass after the loop in the same kernel still cost 6 % (A/B on MI355X, config 5 with
 // counters: in-loop call 123, pass after the loop 129, no pass 137 Gpps; PERPOD unchanged by
 // any of it, so it keeps the call). A launch that deferred a packet writes its number into its
-// stream's mark word (device.hpp StreamSlots, DevTableSet any_mark / any_seq); the k_conn_any
+// stream's mark word (device.hpp StreamSlots, DevTableSet any_mark / any_seq); the k_node_any
 // launched after it on that stream classifies the batch's ANY-protocol packets when the word
 // holds its number, and returns at once otherwise -- stream order makes the word this launch's.
 #ifndef PG_CONN_DEFER_ANY
 #define PG_CONN_DEFER_ANY 1
 #endif
+// PERPOD over a uniform node likewise (k_node_any<1>): without the fallback call the kernel needs
+// no call frame, its SGPR block and the VGPRs the call saved (67 -> 64, no scratch)
+#ifndef PG_POD_DEFER_ANY
+#define PG_POD_DEFER_ANY 0
+#endif
+#ifndef PG_PROBE_NOANYLAUNCH
+#define PG_PROBE_NOANYLAUNCH 0
+#endif
+template <int MODE>
+constexpr bool defer_any() { return MODE == 2 ? PG_CONN_DEFER_ANY : (MODE == 1 ? PG_POD_DEFER_ANY : false); }
 // any of the four protocol bytes of w above 2 (bytes >= 0x80 by their top bit, the rest by a
 // carry-free add into it)
 __device__ __forceinline__ bool any_proto_gt2(uint32_t w) {
     return ((((w & 0x7F7F7F7Fu) + 0x7D7D7D7Du) | w) & 0x80808080u) != 0u;
 }
 
-template <bool COUNT>
-__global__ __launch_bounds__(kBlock) void k_conn_any(DevTableSet T, const uint32_t* __restrict__ src,
+template <int MODE, bool COUNT>
+__global__ __launch_bounds__(kBlock) void k_node_any(DevTableSet T, const uint32_t* __restrict__ src,
                                                   const uint32_t* __restrict__ dst, const uint8_t* __restrict__ proto,
                                                   uint64_t n, uint32_t* __restrict__ out, unsigned long long* counters) {
     if (*T.any_mark != T.any_seq) return;
     const Hist h{nullptr, counters};  // global increments (rare packets)
     const uint64_t stride = (uint64_t)gridDim.x * kBlock;
     for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride)
-        if (proto[i] > 2u) out[i] = conn_any_1<COUNT>(T, src[i], dst[i], h);
+        if (proto[i] > 2u) out[i] = MODE == 2 ? conn_any_1<COUNT>(T, src[i], dst[i], h) : pod_any_1<COUNT>(T, src[i], dst[i], h);
 }
 #ifndef PG_TPL  // tuples per lane per loop iteration (4 or 8)
 #define PG_TPL 4
@@ -586,10 +596,21 @@ constexpr int kernel_wpe() {
     return !NODE ? (MODE == 0 && ((STAGE & 7) == 0 || (STAGE & 7) == 2) ? PG_SINGLE_HBM_WPE : 1)
                  : (node_wide<MODE, COUNT, NODE, STAGE>() ? PG_CONN_COUNT_WPE : PG_NODE_WPE);
 }
+// the most waves per SIMD the register scheduler should aim for: the node builds that are not
+// register-capped are LDS-bound at three 512-thread workgroups per CU (6 waves per SIMD), so more
+// than 6 buys nothing and only costs the scheduler latency hiding (PG_NODE_WPE_MAX)
+#ifndef PG_NODE_WPE_MAX
+#define PG_NODE_WPE_MAX 8
+#endif
+template <int MODE, bool COUNT, bool NODE, int STAGE = 1>
+constexpr int kernel_wpe_max() {
+    return NODE && !node_wide<MODE, COUNT, NODE, STAGE>() ? PG_NODE_WPE_MAX : 8;
+}
 // STAGE_ + 8 (SINGLE, STAGE 0-2): the table is dst-free (kFlagDstFree: no rule tests dst), so
 // the dst stream is not read
 template <int MODE, bool COUNT, bool VEC, int STAGE_, bool NODE, int BS>
-__global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(kernel_wpe<MODE, COUNT, NODE, STAGE_>())))
+__global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(kernel_wpe<MODE, COUNT, NODE, STAGE_>(),
+                                                                    kernel_wpe_max<MODE, COUNT, NODE, STAGE_>())))
 void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
                                                      const uint32_t* __restrict__ dst,
                                                      const uint16_t* __restrict__ sport,
@@ -606,8 +627,9 @@ void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
     constexpr bool NOPAIR = NODE && (STAGE_ & 32);
     // STAGE_ + 64 (node kernels): the node's uniform cross layout (DevNode uniform; with + 32)
     constexpr bool UNIF = NODE && NOPAIR && (STAGE_ & 64);
-    // CONN over a uniform node: ANY-protocol packets deferred past the main loop (PG_CONN_DEFER_ANY)
-    constexpr bool DEFER = UNIF && MODE == 2 && PG_CONN_DEFER_ANY;
+    // PERPOD / CONN over a uniform node: ANY-protocol packets deferred to k_node_any
+    // (PG_CONN_DEFER_ANY, PG_POD_DEFER_ANY)
+    constexpr bool DEFER = UNIF && defer_any<MODE>();
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     uint32_t* hist = smem + (STAGE ? stage_words : 0u);
     // node kernels: the LDS histogram, when used, holds every slot (HistT<true>: no window test)
@@ -735,7 +757,7 @@ void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
     auto run_group = [&](const Group& g, uint64_t qq, auto&& hk) {
         uint32_t sv[P], dv[P], spv[P], dpv[P], prv[P], o[P];
         // (DEFER) a protocol code > 2 among the group's: this launch's number into its stream's
-        // mark word for k_conn_any (one test of the packed protocol word per group, no state
+        // mark word for k_node_any (one test of the packed protocol word per group, no state
         // across groups)
         if constexpr (DEFER) {
             bool any = false;
@@ -826,7 +848,7 @@ void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
         out[i] = o[0];
         if (DEFER && pr1[0] > 2u) *T.any_mark = T.any_seq;
     }
-    // (the packets deferred above -- ANY protocol, rare -- are classified by k_conn_any, launched
+    // (the packets deferred above -- ANY protocol, rare -- are classified by k_node_any, launched
     // after this kernel on the same stream)
     if (COUNT) {
         h.flush_hot();
@@ -1055,14 +1077,16 @@ static void launch_bs(const DevTableSet& T, const Tuning& tu, int t, const uint3
     // three times; with counters no difference): fewer streams in flight per CU contend less
     const uint32_t bpc = tu.blocks_per_cu ? tu.blocks_per_cu : (MODE == 0 && (STAGE & 7) == 4 && !COUNT ? 2u : 0u);
     const size_t lds = hist + (size_t)stage * 4;
-    // CONN over a uniform node: k_conn_any after the classify kernel, for its deferred
-    // ANY-protocol packets (PG_CONN_DEFER_ANY; the launch's mark word and number: dev_classify)
-    constexpr bool defer = MODE == 2 && NODE && (STAGE & 32) && (STAGE & 64) && PG_CONN_DEFER_ANY;
+    // PERPOD / CONN over a uniform node: k_node_any after the classify kernel, for its deferred
+    // ANY-protocol packets (PG_CONN_DEFER_ANY, PG_POD_DEFER_ANY; the launch's mark word and
+    // number: dev_classify)
+    constexpr bool defer = NODE && (STAGE & 32) && (STAGE & 64) && defer_any<MODE>();
     hipLaunchKernelGGL(k, dim3(grid_resident(k, BS, lds, items, bpc)), dim3(BS), lds, st, T, t, src, dst, sport, dport,
                        proto, n, out, counters, stage, cells);
-    if constexpr (defer)
-        hipLaunchKernelGGL(k_conn_any<COUNT>, dim3(grid_for(n)), dim3(kBlock), 0, st, T, src, dst, proto, n, out,
-                           counters);
+    if constexpr (defer && !PG_PROBE_NOANYLAUNCH) {  // (measurement build: -DPG_PROBE_NOANYLAUNCH=1 skips it)
+        auto ka = k_node_any<MODE, COUNT>;
+        hipLaunchKernelGGL(ka, dim3(grid_for(n)), dim3(kBlock), 0, st, T, src, dst, proto, n, out, counters);
+    }
 }
 
 // Workgroup size: a staged image is shared by the workgroup, so larger workgroups hold more
@@ -1213,13 +1237,25 @@ static void launch_classify(const DevTableSet& T, const Tuning& tu, int t, const
     }
 }
 
+// A/B variant builds (make variant DEFS=-DPG_ONLY_MODE=1): only one mode's kernels are compiled
+// (a fraction of the full build's time); other modes' launches fail with PG_EIO
+#ifndef PG_ONLY_MODE
+#define PG_ONLY_MODE -1
+#endif
+constexpr bool mode_built(int mode) { return PG_ONLY_MODE < 0 || PG_ONLY_MODE == mode; }
+#ifndef PG_ONLY_NOCOUNT
+#define PG_ONLY_NOCOUNT 0
+#endif
+
 template <int MODE>
 static void dispatch_mode(bool count, bool vec, const DevTableSet& T, const Tuning& tu, int t, const uint32_t* src,
                           const uint32_t* dst, const uint16_t* sport, const uint16_t* dport, const uint8_t* proto,
                           uint64_t n, uint32_t* out, unsigned long long* counters, hipStream_t st) {
     if (count) {
-        if (vec) launch_classify<MODE, true, true>(T, tu, t, src, dst, sport, dport, proto, n, out, counters, st);
-        else launch_classify<MODE, true, false>(T, tu, t, src, dst, sport, dport, proto, n, out, counters, st);
+        if constexpr (PG_ONLY_MODE < 0 || !PG_ONLY_NOCOUNT) {  // (A/B builds: -DPG_ONLY_NOCOUNT=1 leaves these out)
+            if (vec) launch_classify<MODE, true, true>(T, tu, t, src, dst, sport, dport, proto, n, out, counters, st);
+            else launch_classify<MODE, true, false>(T, tu, t, src, dst, sport, dport, proto, n, out, counters, st);
+        }
     } else {
         if (vec) launch_classify<MODE, false, true>(T, tu, t, src, dst, sport, dport, proto, n, out, counters, st);
         else launch_classify<MODE, false, false>(T, tu, t, src, dst, sport, dport, proto, n, out, counters, st);
@@ -1230,8 +1266,8 @@ int dev_classify(const DevTableSet& T, const Tuning& tu, int mode, int table_id,
                  const uint32_t* dst, const uint16_t* sport, const uint16_t* dport, const uint8_t* proto, uint64_t n,
                  uint32_t* out, unsigned long long* counters, void* stream, std::string* err) {
     if (n == 0) return 0;
-    if (mode == 2 && !T.any_mark) {  // (a CONN build may defer packets to k_conn_any: dev_any_mark)
-        if (err) *err = "CONN launch without a launch-mark word";
+    if (mode != 0 && !T.any_mark) {  // (a node build may defer packets to k_node_any: dev_any_mark)
+        if (err) *err = "PERPOD / CONN launch without a launch-mark word";
         return -1;
     }
     auto al = [](const void* p, uintptr_t a) { return ((uintptr_t)p & (a - 1)) == 0; };
@@ -1242,9 +1278,17 @@ int dev_classify(const DevTableSet& T, const Tuning& tu, int mode, int table_id,
                      (mode != 2 || al(sport, kPort));
     hipStream_t st = (hipStream_t)stream;
     const bool count = counters != nullptr;
-    if (mode == 0) dispatch_mode<0>(count, vec, T, tu, table_id, src, dst, sport, dport, proto, n, out, counters, st);
-    else if (mode == 1) dispatch_mode<1>(count, vec, T, tu, table_id, src, dst, sport, dport, proto, n, out, counters, st);
-    else dispatch_mode<2>(count, vec, T, tu, table_id, src, dst, sport, dport, proto, n, out, counters, st);
+    if (!mode_built(mode)) {
+        if (err) *err = "this build (PG_ONLY_MODE) has no kernels for mode " + std::to_string(mode);
+        return -1;
+    }
+    if (mode == 0) {
+        if constexpr (mode_built(0)) dispatch_mode<0>(count, vec, T, tu, table_id, src, dst, sport, dport, proto, n, out, counters, st);
+    } else if (mode == 1) {
+        if constexpr (mode_built(1)) dispatch_mode<1>(count, vec, T, tu, table_id, src, dst, sport, dport, proto, n, out, counters, st);
+    } else {
+        if constexpr (mode_built(2)) dispatch_mode<2>(count, vec, T, tu, table_id, src, dst, sport, dport, proto, n, out, counters, st);
+    }
     HIPCHK(hipGetLastError());
     return 0;
 }

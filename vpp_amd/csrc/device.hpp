@@ -101,6 +101,11 @@ struct DevNode {
     // one uint2 mask per IP class in its record (bit t: that class's row of table t is the
     // common one; class g's at word cmap + (g << cmap_shift))
     uint32_t uniform, crow0;
+    uint32_t tstride;      // uniform layout: cross words per table, n_ipc * gk (below 2^24)
+    // list-verdict table (Tuning::node_list_table; 0 = the record form above): a kNodeList word's
+    // low bits are a list id L, and its verdict for the rule's dst-side address is cross word
+    // lv0 + L * n_ipc + (that address's node IP class) -- one gather, no record walk
+    uint32_t lv0;
 };
 
 // table sets of up to this many counter slots are counted by a full LDS histogram (one cell per
@@ -119,13 +124,13 @@ constexpr int32_t kEndRemote = 1 << 28, kEndInet = 2 << 28;
 constexpr uint32_t kEndKindShift = 28;
 
 // Streams that launched kernels reading one table set, one slot each (device.hip DeviceBuffers:
-// the slot's completion events, and its CONN launch-mark word). A CONN launch over a uniform node
-// defers its ANY-protocol packets to k_conn_any, launched after it on the same stream
+// the slot's completion events, and its launch-mark word). A PERPOD / CONN launch over a uniform
+// node defers its ANY-protocol packets to k_node_any, launched after it on the same stream
 // (device.hip PG_CONN_DEFER_ANY): the classify kernel writes its launch number into its
-// stream's mark word when it deferred a packet, and k_conn_any runs only when the word holds its
+// stream's mark word when it deferred a packet, and k_node_any runs only when the word holds its
 // own number. Both launches are on one stream, so stream order alone makes the mark the one of
 // this launch; a stale number (an earlier launch, or a slot reassigned after clear()) can only
-// equal a later launch's after 2^32 - 1 more draws, and then k_conn_any makes a pass that finds
+// equal a later launch's after 2^32 - 1 more draws, and then k_node_any makes a pass that finds
 // nothing to do -- never a skipped packet. Host-only bookkeeping, tested without a GPU
 // (pg_debug_stream_slots).
 struct StreamSlots {
@@ -168,7 +173,7 @@ struct DevTableSet {       // device pointers (valid on the GPU)
     // ACL", in a register
     uint32_t slot_hot_in;
     DevNode node;
-    // CONN launches: the launch stream's mark word and this launch's number (StreamSlots; set per
+    // PERPOD / CONN launches: the launch stream's mark word and this launch's number (StreamSlots; set per
     // launch by pg_classify through dev_any_mark, null otherwise)
     uint32_t* any_mark;
     uint32_t any_seq;
@@ -192,6 +197,7 @@ struct HostTableSet {
     std::vector<uint32_t> node_img, node_cross;  // empty img: no node classifier
     DevNode node{};                              // header fields (pointers unset)
     uint32_t node_rec_words = 0;                 // words of the node's dst records (build_node)
+    uint32_t node_list_tab_words = 0;            // words of its list-verdict table (DevNode lv0)
 };
 
 // table blobs up to this many words are staged in LDS by default (64 KiB); larger ones are
@@ -219,6 +225,7 @@ struct Tuning {
                                       // of node launches whose set has more slots than the LDS histogram
     uint32_t node_list_words = 4096;  // node dst records up to this many words go into the image (0 = never)
     uint32_t node_uniform = 1;        // the node's uniform cross layout where it applies (DevNode uniform)
+    uint32_t node_list_table = 1;     // node lists resolved by a list-verdict table (DevNode lv0), else records
     // launches
     uint32_t blocks_per_cu = 0;    // cap on resident workgroups per CU (0 = occupancy)
     uint32_t stage_max_words = kStageBlobWords;  // table blobs staged whole in LDS

@@ -57,6 +57,7 @@ const Knob kKnobs[] = {
     {"node_hist_cells", &Tuning::node_hist_cells, 0, 8192, false},
     {"node_list_words", &Tuning::node_list_words, 0, 16384, true},
     {"node_uniform", &Tuning::node_uniform, 0, 1, true},
+    {"node_list_table", &Tuning::node_list_table, 0, 1, true},
     {"blocks_per_cu", &Tuning::blocks_per_cu, 0, 64, false},
     {"stage_max_words", &Tuning::stage_max_words, 0, 36864, false},
     {"node_stage_max_words", &Tuning::node_stage_max_words, 0, 36864, false},

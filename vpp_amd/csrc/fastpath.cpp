@@ -157,6 +157,7 @@ constexpr uint32_t kPairMaxRules = 1u << 16;
 constexpr uint64_t kPairBudget = 1ull << 22;  // entries of each PAIR phase table (16 MiB)
 constexpr size_t kPairListMin = 16;  // CROSS dst lists longer than this: PAIR instead
 constexpr uint64_t kNodeCrossBudget = 1ull << 25;  // node cross entries (128 MiB)
+constexpr uint64_t kNodeListTabBudget = 1ull << 24;  // node list-verdict entries (64 MiB)
 
 }  // namespace
 
@@ -933,11 +934,51 @@ bool build_node(HostTableSet& h, const std::vector<TableAnalysis*>& an, const st
     std::vector<size_t> pcov;  // indices into cov
     for (size_t c = 0; c < cov.size(); c++)
         if (an[cov[c]]->pair) pcov.push_back(c);
+    // List tables (cross-product tables with dst-specific rules in front of some verdicts,
+    // clist): with Tuning::node_list_table the IPv4 partition also separates every address
+    // range those rules' dst prefixes tell apart (the class key holds, per list table, which of
+    // them contain the class), so a list resolves by the rule-dst-side address's class alone: one
+    // entry of a list-verdict table [list][node IP class] instead of a walk over its records
+    std::vector<size_t> lcov;  // indices into cov
+    std::vector<std::vector<uint64_t>> lb;   // per list table: its dst interval starts
+    std::vector<std::vector<uint32_t>> lcl;  // ... and their classes (set of containing prefixes)
+    if (tu.node_list_table)
+        for (size_t c = 0; c < cov.size(); c++) {
+            const TableAnalysis& A = *an[cov[c]];
+            if (A.pair) continue;
+            std::vector<uint32_t> lr;  // the table's list rules
+            for (const auto& l : A.clist) lr.insert(lr.end(), l.begin(), l.end());
+            if (lr.empty()) continue;
+            std::sort(lr.begin(), lr.end());
+            lr.erase(std::unique(lr.begin(), lr.end()), lr.end());
+            std::vector<uint64_t> b{0};
+            for (uint32_t r : lr) {
+                const DevRule& R = A.rules[r];
+                b.push_back(R.dnet & R.dmask);
+                b.push_back((uint64_t)(R.dnet & R.dmask) + (uint64_t)(~R.dmask) + 1u);
+            }
+            std::sort(b.begin(), b.end());
+            b.erase(std::unique(b.begin(), b.end()), b.end());
+            while (!b.empty() && b.back() >= (1ull << 32)) b.pop_back();
+            std::map<std::vector<uint32_t>, uint32_t> ids;
+            std::vector<uint32_t> cl(b.size());
+            std::vector<uint32_t> in;
+            for (size_t k = 0; k < b.size(); k++) {
+                in.clear();
+                for (uint32_t r : lr)
+                    if (((uint32_t)b[k] & A.rules[r].dmask) == (A.rules[r].dnet & A.rules[r].dmask)) in.push_back(r);
+                cl[k] = ids.emplace(in, (uint32_t)ids.size()).first->second;
+            }
+            lcov.push_back(c);
+            lb.push_back(std::move(b));
+            lcl.push_back(std::move(cl));
+        }
 
     // IPv4 partition
     std::vector<uint64_t> gb{0};
     for (uint32_t t : cov) gb.insert(gb.end(), an[t]->sb.begin(), an[t]->sb.end());
     for (size_t c : pcov) gb.insert(gb.end(), an[cov[c]]->db.begin(), an[cov[c]]->db.end());
+    for (const auto& b : lb) gb.insert(gb.end(), b.begin(), b.end());
     if ((uint64_t)h.rules.size() + T + 2 >= kNodeList) return false;  // verdict slots below the list flag
     std::map<uint32_t, NodePod> by_ip;  // a repeated address: the last pod wins, as in the iphash
     for (const NodePod& p : pods) by_ip[p.ip] = p;
@@ -951,13 +992,16 @@ bool build_node(HostTableSet& h, const std::vector<TableAnalysis*>& an, const st
     gb.erase(std::unique(gb.begin(), gb.end()), gb.end());
     const size_t C = cov.size();
     const size_t PC = pcov.size();
-    std::vector<size_t> at(C, 0), atd(PC, 0);
+    const size_t LC = lcov.size();
+    std::vector<size_t> at(C, 0), atd(PC, 0), atl(LC, 0);
     std::unordered_map<std::vector<uint32_t>, uint32_t, VecHash> ipc_of;
-    // class -> {ifc, tin, tout, src class per covered table..., dst class per PAIR table...}
+    // class -> {ifc, tin, tout, src class per covered table..., dst class per PAIR table...,
+    // list-dst class per list table...}
     std::vector<std::vector<uint32_t>> ipc_key;
+    std::vector<uint32_t> ipc_rep;  // per class: an address in it (list verdicts)
     std::vector<uint32_t> gcls(gb.size());
     size_t pi = 0;
-    std::vector<uint32_t> key(3 + C + PC);
+    std::vector<uint32_t> key(3 + C + PC + LC);
     for (size_t k = 0; k < gb.size(); k++) {
         const uint64_t a = gb[k];
         while (pi < ps.size() && ps[pi].ip < a) pi++;
@@ -973,10 +1017,15 @@ bool build_node(HostTableSet& h, const std::vector<TableAnalysis*>& an, const st
             while (atd[q] + 1 < A.db.size() && A.db[atd[q] + 1] <= a) atd[q]++;
             key[3 + C + q] = A.dint_cls[atd[q]];
         }
+        for (size_t q = 0; q < LC; q++) {
+            while (atl[q] + 1 < lb[q].size() && lb[q][atl[q] + 1] <= a) atl[q]++;
+            key[3 + C + PC + q] = lcl[q][atl[q]];
+        }
         auto it = ipc_of.find(key);
         if (it == ipc_of.end()) {
             it = ipc_of.emplace(key, (uint32_t)ipc_key.size()).first;
             ipc_key.push_back(key);
+            ipc_rep.push_back((uint32_t)a);
         }
         gcls[k] = it->second;
     }
@@ -1076,8 +1125,10 @@ bool build_node(HostTableSet& h, const std::vector<TableAnalysis*>& an, const st
             slot[g] = nx, used[nx] = 1;
         }
         std::vector<std::vector<uint32_t>> rk(S, ipc_key[0]);
-        for (uint32_t g = 0; g < G; g++) rk[slot[g]] = ipc_key[g];
+        std::vector<uint32_t> rr(S, ipc_rep[0]);
+        for (uint32_t g = 0; g < G; g++) rk[slot[g]] = ipc_key[g], rr[slot[g]] = ipc_rep[g];
         ipc_key.swap(rk);
+        ipc_rep.swap(rr);
         std::vector<std::pair<uint32_t, uint32_t>> lv;
         node_trie_leaves(img, 0, N.ip_s1, true, [&](uint32_t pos, uint32_t c, uint32_t) { lv.push_back({pos, c}); });
         for (auto& x : lv) img[x.first] = kLeaf | slot[x.second];
@@ -1090,7 +1141,8 @@ bool build_node(HostTableSet& h, const std::vector<TableAnalysis*>& an, const st
         entries += an[t]->pair ? (uint64_t)an[t]->nsc * an[t]->ndc + (uint64_t)an[t]->npc * an[t]->nkc
                                : (uint64_t)G * an[t]->nkc;
     if (entries > kNodeCrossBudget) return false;
-    const bool uni = aligned && (uint64_t)T * G < (1u << 24) && (uint64_t)T * G * GK <= kNodeCrossBudget;
+    const bool uni = aligned && (uint64_t)T * G < (1u << 24) && (uint64_t)T * G * GK <= kNodeCrossBudget &&
+                     (uint64_t)G * GK < (1u << 24);  // (24-bit products: classify.hpp mad24)
     if (aligned && !uni) {  // (the aligned tries are the uniform layout's): the other layout
         Tuning t2 = tu;
         t2.node_uniform = 0;
@@ -1183,11 +1235,16 @@ bool build_node(HostTableSet& h, const std::vector<TableAnalysis*>& an, const st
     N.img_words = N.img_words_base = (uint32_t)img.size();
     N.cmap = 0;
 
-    // cross entries, then the dst records of the pairs with a list
+    // cross entries, then the dst records of the pairs with a list (or the list-verdict table)
     std::vector<uint32_t>& X = h.node_cross;
     X.reserve(entries + 16);
     std::vector<uint32_t> recs;
     const size_t rec0 = (entries + 3) & ~(uint64_t)3;
+    const bool ltab = tu.node_list_table != 0;  // (every list table is in lcov then)
+    struct ListRef {
+        size_t c, e;  // the list of (covered table cov[c], src class x key class e)
+    };
+    std::vector<ListRef> lists;
     size_t q = 0;
     for (size_t c = 0; c < C; c++) {
         const uint32_t t = cov[c];
@@ -1217,7 +1274,11 @@ bool build_node(HostTableSet& h, const std::vector<TableAnalysis*>& an, const st
                     X.push_back(A.cverd[e]);
                     continue;
                 }
-                if (first[e] == 0xFFFFFFFFu) {
+                if (first[e] == 0xFFFFFFFFu && ltab) {  // list id
+                    if (lists.size() >= kNodeRecMask) return false;
+                    first[e] = (uint32_t)lists.size();
+                    lists.push_back(ListRef{c, e});
+                } else if (first[e] == 0xFFFFFFFFu) {
                     const uint64_t ri = (rec0 + recs.size()) / 4;
                     if (ri >= kNodeRecMask) return false;
                     first[e] = (uint32_t)ri;
@@ -1242,9 +1303,39 @@ bool build_node(HostTableSet& h, const std::vector<TableAnalysis*>& an, const st
         if (!an[t]->pair) xcov.push_back(t);
     build_common_rows(h, xcov, an, tu, uni);
     N.uniform = uni;
+    N.tstride = uni ? G * GK : 0;
     N.crow0 = uni && N.cmap ? img[N.tabinfo + 2] : 0;  // table 0's common row: table t's at crow0 + t * GK
     X.resize(rec0, 0);
     X.insert(X.end(), recs.begin(), recs.end());
+    // list-verdict table (DevNode lv0): list L's verdict for node IP class g at lv0 + L * G + g --
+    // its first rule whose dst prefix contains the class (every address of a class lies in the
+    // same prefixes of every list table: the class key), else the verdict behind the list
+    N.lv0 = 0;
+    h.node_list_tab_words = 0;
+    if (!lists.empty()) {
+        if ((uint64_t)lists.size() * G > kNodeListTabBudget) {  // the record form instead
+            Tuning t2 = tu;
+            t2.node_list_table = 0;
+            return build_node(h, an, pods, node_end, t2);
+        }
+        N.lv0 = (uint32_t)X.size();
+        h.node_list_tab_words = (uint32_t)(lists.size() * G);
+        X.reserve(X.size() + lists.size() * G);
+        for (const ListRef& L : lists) {
+            const TableAnalysis& A = *an[cov[L.c]];
+            for (uint32_t g = 0; g < G; g++) {
+                uint32_t v = A.cverd[L.e];
+                for (uint32_t r : A.clist[L.e]) {
+                    const DevRule& R = A.rules[r];
+                    if ((ipc_rep[g] & R.dmask) == R.dnet) {
+                        v = ((R.act & 3u) << 30) | (A.rule_base + r);
+                        break;
+                    }
+                }
+                X.push_back(v);
+            }
+        }
+    }
     // dst records, also at the end of the image when they fit node_list_words: a launch that
     // stages them walks a list in LDS instead of one dependent gather per record (config 3:
     // +17 % with the lists not walked at all, measured); launches that do not stage them read

@@ -333,6 +333,9 @@ class Engine:
         rb, inimg = C.c_uint64(), C.c_int()
         self._ck(lib.pg_node_list_stats(self.h, C.byref(rb), C.byref(inimg)))
         st.update(list_record_bytes=rb.value, list_records_in_image=bool(inimg.value))
+        lt = C.c_uint64()
+        self._ck(lib.pg_node_list_table_stats(self.h, C.byref(lt)))
+        st.update(list_table_bytes=lt.value)
         st.update(uniform=bool(self._ck(lib.pg_node_uniform(self.h))))
         return st
 
