@@ -158,7 +158,8 @@ int pg_ctx_device(const pg_ctx* ctx);
  * table compiler (the context recompiles and re-uploads on its next use; hit counters carry over)
  * -- "root_bits_max" (cap of the src/key trie root stride, 4..16, default 16), "node_build"
  * (1/0: build the node classifier for PERPOD / CONN, default 1), "node_root_bits" (its IPv4 /
- * key trie root stride cap, default 12), "lc_lds" (table blobs of at least this many words are
+ * key trie root stride cap, default 12), "node_key_root_bits" (cap of the uniform layout's
+ * key trie root stride: 2, 6 or 10 bits -- 10 saves a level for ~4 KiB of image; default 8), "lc_lds" (table blobs of at least this many words are
  * rebuilt with level-compressed 12/16-bit trie strides and keep them when the result still
  * fits in LDS; default 4096, 0 = off; blobs too large for LDS are always level-compressed),
  * "lc_dense12" (boundaries a subtree needs for a 12-bit stride, default 16), "lc_max_stride"

@@ -637,8 +637,8 @@ PG_HD void node_trie2_q(const L& ld, const DevNode& N, const uint32_t (&a)[QA], 
 
 // node_trie2_q, with the tries' shape as compile-time constants when it is one of the common ones
 // of the uniform layout (aligned tries: IPv4 root 8 bits + three 8-bit levels; key root 6 bits +
-// 8 + 4, or 2 bits + 8 + 8 -- fastpath.cpp build_node picks the fewest levels, then the smallest
-// image), else read at run time. The shape test is uniform (a scalar branch).
+// 8 + 4, 2 bits + 8 + 8, or 10 bits + 8 -- fastpath.cpp build_node picks the fewest levels, then
+// the smallest image), else read at run time. The shape test is uniform (a scalar branch).
 template <bool PRED, bool A, class L, int QA, int QB>
 PG_HD void node_walks(const L& ld, const DevNode& N, const uint32_t (&a)[QA], uint32_t (&rr)[QA],
                       const uint32_t (&b)[QB], uint32_t (&cb)[QB]) {
@@ -648,6 +648,8 @@ PG_HD void node_walks(const L& ld, const DevNode& N, const uint32_t (&a)[QA], ui
             return node_trie2_q<PRED, A, 8, 4, 6, 3>(ld, N, a, rr, b, cb);
         if (shape == (8u | 4u << 8 | 2u << 16 | 3u << 24))
             return node_trie2_q<PRED, A, 8, 4, 2, 3>(ld, N, a, rr, b, cb);
+        if (shape == (8u | 4u << 8 | 10u << 16 | 2u << 24))
+            return node_trie2_q<PRED, A, 8, 4, 10, 2>(ld, N, a, rr, b, cb);
     }
     node_trie2_q<PRED, A>(ld, N, a, rr, b, cb);
 }

@@ -518,8 +518,11 @@ __global__ __launch_bounds__(kBlock) void k_node_any(DevTableSet T, const uint32
 #ifndef PG_TPL  // tuples per lane per loop iteration (4 or 8)
 #define PG_TPL 4
 #endif
-#ifndef PG_TPL_CONN  // ... in CONN mode: 8 (A/B on MI355X, config 5 with counters 133.7 -> 137.7 Gpps,
-#define PG_TPL_CONN 8  // without 163.3 -> 165.7; PERPOD and SINGLE lose at 8: config 3 334 -> 238)
+// ... in CONN mode: 4 (round 4 measured 8 ahead, 133.7 -> 137.7 Gpps for config 5 with counters;
+// with the node walks' compile-time shapes (classify.hpp node_walks) 8 tuples per lane no longer
+// fit the 64-register cap of the CONN build: 144 B of scratch per lane, 109 Gpps, vs 142 at 4)
+#ifndef PG_TPL_CONN
+#define PG_TPL_CONN 4
 #endif
 template <int MODE>
 constexpr int tuples_per_lane() { return MODE == 2 ? PG_TPL_CONN : PG_TPL; }

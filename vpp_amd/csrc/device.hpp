@@ -217,6 +217,10 @@ struct Tuning {
     uint32_t pair = 1;             // PAIR for tables CROSS cannot take (0 = CAND, 2 = wherever it fits)
     uint32_t node_build = 1;       // build the node classifier (PERPOD / CONN)
     uint32_t node_root_bits = 12;  // its IPv4 / key trie root stride cap (4..16)
+    // uniform layout: cap of the key trie's root stride (2, 6 or 10). 10 saves a level (config 3
+    // +1 % in the driver's window) but its 4 KiB push config 5's image + counter histogram past
+    // the 80 KiB that keep two 1024-thread workgroups per CU (139 -> 94 Gpps)
+    uint32_t node_key_root_bits = 8;
     uint32_t node_common = 1;      // common-row section of node images
     uint32_t fd = 1;               // FD form of dst-independent CROSS tables that fit LDS
     uint32_t candi = 1;            // CANDI form (inline candidates) of dst-independent HBM-resident CAND tables

@@ -50,6 +50,7 @@ const Knob kKnobs[] = {
     {"pair", &Tuning::pair, 0, 2, true},
     {"node_build", &Tuning::node_build, 0, 1, true},
     {"node_root_bits", &Tuning::node_root_bits, 4, 16, true},
+    {"node_key_root_bits", &Tuning::node_key_root_bits, 2, 10, true},
     {"node_common", &Tuning::node_common, 0, 1, true},
     {"fd", &Tuning::fd, 0, 1, true},
     {"candi", &Tuning::candi, 0, 1, true},

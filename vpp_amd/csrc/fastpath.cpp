@@ -1149,14 +1149,13 @@ bool build_node(HostTableSet& h, const std::vector<TableAnalysis*>& an, const st
         return build_node(h, an, pods, node_end, t2);
     }
     if (uni) entries = (uint64_t)T * G * GK;
-    // L4-key trie: aligned, the root stride (18 - root a multiple of 4, at most 8 bits: a 10-bit
-    // root saves a level but its 4 KiB cost config 3 a workgroup per CU) with the fewest levels,
-    // then the smallest trie
+    // L4-key trie: aligned, the root stride (18 - root a multiple of 4, at most
+    // Tuning::node_key_root_bits) with the fewest levels, then the smallest trie
     if (aligned) {
         const size_t k0 = img.size();
         std::vector<uint32_t> best;
         uint32_t best_d = ~0u;
-        for (uint32_t k1 = 2; k1 <= std::min(tu.node_root_bits, 8u); k1 += 4) {
+        for (uint32_t k1 = 2; k1 <= std::min(tu.node_root_bits, tu.node_key_root_bits); k1 += 4) {
             img.resize(k0);
             const uint32_t root = build_trie(img, kb, kcls, 18, k1, tu, false, enc, kNodeStride);
             if (root == kTrieFail) continue;
