@@ -813,8 +813,8 @@ struct NodeEval {
             pos[j] = (w[j] & kNodeRecMask) << 2;
         }
         // list-verdict table (N.lv0): one read at [list][node IP class of the rule's dst-side
-        // address] (fastpath.cpp build_node)
-        if (N.lv0) {
+        // address] (fastpath.cpp build_node; the only list form of the uniform layout)
+        if (UNI || N.lv0) {
             const uint32_t(&cb)[Q] = rev ? cs : cd;
             PG_UNROLL
             for (int j = 0; j < Q; j++)
@@ -843,8 +843,10 @@ struct NodeEval {
                 }
             }
         };
-        if (N.lrec) walk(img, N.lrec - N.rec0);
-        else walk(X, 0u);
+        if constexpr (!UNI) {
+            if (N.lrec) walk(img, N.lrec - N.rec0);
+            else walk(X, 0u);
+        }
         bool anyfb = false;
         PG_UNROLL
         for (int j = 0; j < Q; j++) anyfb |= fb[j];

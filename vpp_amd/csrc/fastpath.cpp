@@ -1075,7 +1075,11 @@ bool build_node(HostTableSet& h, const std::vector<TableAnalysis*>& an, const st
     // aligned encoding (blobwalk.hpp: one VALU less per step, strides of 8 and 4 only); other
     // node sets the shifted one, whose strides are free (config 6: a 4-KiB smaller image keeps
     // three workgroups per CU)
-    const bool aligned = tu.node_uniform && C == T && PC == 0 && T <= 64 && pack_ok;
+    // (and it resolves lists by the list-verdict table: its kernels carry no record walk)
+    bool has_lists = false;
+    for (uint32_t t : cov)
+        for (const auto& l : an[t]->clist) has_lists |= !l.empty();
+    const bool aligned = tu.node_uniform && C == T && PC == 0 && T <= 64 && pack_ok && (tu.node_list_table || !has_lists);
     const int enc = aligned ? kEncNodeA : kEncNode;
     // IPv4 trie root: the smallest trie among the root strides that give the fewest levels (a
     // walk reads exactly depth words; a smaller image leaves LDS for the counter histogram --
@@ -1312,9 +1316,10 @@ bool build_node(HostTableSet& h, const std::vector<TableAnalysis*>& an, const st
     N.lv0 = 0;
     h.node_list_tab_words = 0;
     if (!lists.empty()) {
-        if ((uint64_t)lists.size() * G > kNodeListTabBudget) {  // the record form instead
+        if ((uint64_t)lists.size() * G > kNodeListTabBudget) {  // the record form instead (not uniform)
             Tuning t2 = tu;
             t2.node_list_table = 0;
+            t2.node_uniform = 0;
             return build_node(h, an, pods, node_end, t2);
         }
         N.lv0 = (uint32_t)X.size();
