@@ -271,24 +271,31 @@ def test_generator_matches_numpy_restatement():
             assert np.array_equal(np.asarray(g), np.asarray(x))
 
 
-@pytest.mark.parametrize("config", [3, 5])
-def test_cluster_configs_gpu_vs_oracle(config):
-    """Configs 3 (PERPOD) and 5 (CONN, with counters) at full topology (1k pods, ~10k rules),
-    2M device-generated tuples, bit-exact against the C oracle through oracle.world."""
+@pytest.mark.parametrize("config,mode", [(3, None), (5, None), (8, None), (8, MODE_CONN)],
+                         ids=["3", "5", "8", "8conn"])
+def test_cluster_configs_gpu_vs_oracle(config, mode):
+    """Configs 3 (PERPOD) and 5 (CONN) at full topology (1k pods, ~10k rules), and config 8 --
+    the same cluster with 20 apps per namespace: 202 per-pod tables, past the 64 one common-row
+    mask bit each covers (grouped marks) -- in both modes; 2M device-generated tuples, with hit
+    counters, bit-exact against the C oracle through oracle.world."""
     from oracle.world import World
     from vpp_amd import workloads as W
     w = W.CONFIGS[config](0, n_tuples=2 << 20)
     e = w.engine
-    b = D.TupleBatch(w.n_tuples, with_sport=(w.mode == MODE_CONN))
+    mode = w.mode if mode is None else mode
+    if config == 8:
+        ns = e.node_stats()
+        assert e.num_tables() > 64 and ns["uniform"] and ns["common_row_pairs"] > 0.5 * ns["table_ipclass_pairs"], ns
+    b = D.TupleBatch(w.n_tuples, with_sport=(mode == MODE_CONN))
     D.gen_tuples(e, b, **w.gen)
     out = torch.empty(b.n, dtype=torch.int32, device="cuda")
     cnt = torch.zeros(e.num_counter_slots(), dtype=torch.int64, device="cuda")
-    D.classify(e, w.mode, -1, b, out, counters=cnt)
+    D.classify(e, mode, -1, b, out, counters=cnt)
     torch.cuda.synchronize()
     got = out.cpu().numpy().view(np.uint32)
     src, dst, sport, dport, proto = b.numpy(b.n)
     wd = World(e, w.local_ifs, w.node_if)
-    if w.mode == MODE_PERPOD:
+    if mode == MODE_PERPOD:
         act, slot = wd.perpod(src, dst, dport, proto, threads=16)
         # one evaluation per tuple: the counters are the histogram of the verdict slots
         assert np.array_equal(cnt.cpu().numpy(), np.bincount(got & 0x3FFFFFFF, minlength=cnt.numel()))

@@ -185,6 +185,30 @@ def test_config3_cluster_node_path():
     assert ns["uniform"], ns
 
 
+def test_config8_more_than_64_tables_uniform_grouped_marks():
+    """Config 8 (config 3's cluster with 20 apps per namespace: 202 per-pod tables, past the
+    64 tables one 64-bit common-row mask per IP class marks one by one): still the uniform
+    layout, its marks cover groups of tables (a clear group bit gathers the entry from the cross
+    table), and PERPOD / CONN with counters equal the oracle and the layout without common rows."""
+    w = W.config8(0, n_tuples=1 << 16)
+    e = w.engine
+    ns = e.node_stats()
+    assert e.num_tables() > 64 and ns["uniform"] and ns["image_bytes"] <= 64 << 10, ns
+    assert ns["common_row_pairs"] >= 0.5 * ns["table_ipclass_pairs"], ns
+    src, dst, sport, dport, proto = gen.gen_tuples(40001, **w.gen)
+    wd = World(e, w.local_ifs, w.node_if)
+    act, slot = wd.perpod(src, dst, dport, proto, threads=8)
+    got, cnt = e.debug_classify_host(MODE_PERPOD, -1, src, dst, sport, dport, proto, node=True, counters=True)
+    assert np.array_equal(got >> 30, act.astype(np.uint32)) and np.array_equal(got & 0x3FFFFFFF, slot)
+    assert np.array_equal(cnt, np.bincount(got & 0x3FFFFFFF, minlength=len(cnt)))
+    conn, cslot, hist = wd.conn(src, dst, sport, dport, proto, threads=8, hist=True)
+    got, cnt = e.debug_classify_host(MODE_CONN, -1, src, dst, sport, dport, proto, node=True, counters=True)
+    assert np.array_equal(got >> 30, conn.astype(np.uint32)) and np.array_equal(got & 0x3FFFFFFF, cslot)
+    assert np.array_equal(cnt, hist)
+    got0 = e.debug_classify_host(MODE_CONN, -1, src, dst, sport, dport, proto, node=True, common=False)
+    assert np.array_equal(got0, got)
+
+
 def test_node_lists_table_or_records_in_image_or_cross():
     """A node cross entry with dst-specific rules ahead of its verdict resolves them the same
     three ways, all equal to the oracle: by the list-verdict table (default: one read at [list]

@@ -759,10 +759,13 @@ int pg_node_common_stats(pg_ctx* ctx, uint64_t* base_image_bytes, uint64_t* comm
     if (h.node_img.empty()) return fail(ctx, PG_ENOENT, "no node classifier (disabled or over budget)");
     uint64_t covered = 0, common = 0;
     for (size_t t = 0; t < h.tabs.size(); t++)
-        if (h.node_img[h.node.tabinfo + 4 * t + 1] >> 31) covered++;
+        if ((h.node.uniform ? h.node_aux : h.node_img)[h.node.tabinfo + 4 * t + 1] >> 31) covered++;
     if (h.node.cmap && h.node.uniform)  // one 64-bit mask per IP class, in the class records
         for (size_t g = 0; g < h.node.n_ipc; g++)
-            for (size_t w = 0; w < 2; w++) common += (uint64_t)__builtin_popcount(h.node_img[h.node.cmap + (g << h.node.cmap_shift) + w]);
+            for (size_t t = 0; t < h.tabs.size(); t++) {
+                const size_t b = t >> h.node.gshift;
+                common += (h.node_img[h.node.cmap + (g << h.node.cmap_shift) + (b >> 5)] >> (b & 31)) & 1u;
+            }
     else if (h.node.cmap)
         for (size_t i = h.node.cmap; i < (h.node.lrec ? h.node.lrec : h.node.img_words); i++) common += (uint64_t)__builtin_popcount(h.node_img[i]);
     if (base_image_bytes) *base_image_bytes = (uint64_t)h.node.img_words_base * 4;

@@ -723,9 +723,10 @@ struct NodeEval {
             for (int j = 0; j < Q; j++) {
                 const uint32_t tt = act[j] ? (uint32_t)t[j] : 0u;
                 uint32_t cw = 0;
-                if (CM) {  // bit t of the rule-src-side class's mask
+                if (CM) {  // bit t (past 64 tables: t's group) of the rule-src-side class's mask
                     const W2 m = rev ? (*msk_d)[j] : (*msk_s)[j];
-                    cw = bit_of(tt < 32u ? m.x : m.y, tt);
+                    const uint32_t tb = tt >> N.gshift;
+                    cw = bit_of(tb < 32u ? m.x : m.y, tb);
                 }
                 on[j] = act[j] && k[j] < kWalkKeyLimit;
                 cm[j] = CM && cw != 0u;

@@ -94,14 +94,15 @@ struct DevNode {
     // (record word p of the cross numbering is image word p - rec0 + lrec); launches that do not
     // stage that part of the image clear lrec and read the cross array
     uint32_t rec0, lrec;
-    // uniform layout (every table covered, none in PAIR form, at most 64 tables;
+    // uniform layout (every table covered, none in PAIR form, fewer than 255 tables;
     // Tuning::node_uniform): table t's cross rows are over the node key classes, entry (t, ip
     // class g, key class k) at word (t * n_ipc + g) * gk + k, and its common row (when cmap != 0)
     // at image word crow0 + t * gk; tabinfo and kmap are not read, and the common-row marks are
-    // one uint2 mask per IP class in its record (bit t: that class's row of table t is the
-    // common one; class g's at word cmap + (g << cmap_shift))
+    // one uint2 mask per IP class in its record (bit t >> gshift: that class's row of table t --
+    // of every table of t's group -- is the common one; class g's at word cmap + (g << cmap_shift))
     uint32_t uniform, crow0;
     uint32_t tstride;      // uniform layout: cross words per table, n_ipc * gk (below 2^24)
+    uint32_t gshift;       // uniform layout: common-row mark bit of table t is t >> gshift (> 64 tables)
     // list-verdict table (Tuning::node_list_table; 0 = the record form above): a kNodeList word's
     // low bits are a list id L, and its verdict for the rule's dst-side address is cross word
     // lv0 + L * n_ipc + (that address's node IP class) -- one gather, no record walk
@@ -195,6 +196,7 @@ struct HostTableSet {
     int32_t node_if = -1, node_in = -1, node_out = -1;
     uint32_t slot_hot_in = 0xFFFFFFFFu;          // DevTableSet.slot_hot_in (engine.cpp compile)
     std::vector<uint32_t> node_img, node_cross;  // empty img: no node classifier
+    std::vector<uint32_t> node_aux;              // uniform layout: tabinfo and kmap (host only)
     DevNode node{};                              // header fields (pointers unset)
     uint32_t node_rec_words = 0;                 // words of the node's dst records (build_node)
     uint32_t node_list_tab_words = 0;            // words of its list-verdict table (DevNode lv0)

@@ -863,6 +863,7 @@ constexpr uint64_t kCommonMapMaxBits = 1ull << 20;  // 128 KiB
 void build_common_rows(HostTableSet& h, const std::vector<uint32_t>& cov, const std::vector<TableAnalysis*>& an,
                        const Tuning& tu, bool uni) {
     std::vector<uint32_t>& img = h.node_img;
+    std::vector<uint32_t>& TI = uni ? h.node_aux : h.node_img;  // tabinfo (build_node)
     DevNode& N = h.node;
     const uint32_t T = (uint32_t)h.tabs.size(), G = N.n_ipc;
     uint32_t rs = 0;  // bitmap row: G bits in 2^rs words
@@ -872,11 +873,18 @@ void build_common_rows(HostTableSet& h, const std::vector<uint32_t>& cov, const 
     const std::vector<uint32_t>& X = h.node_cross;
     std::vector<uint32_t> sec, map(uni ? 0 : (size_t)(bits / 32), 0);
     // uniform layout: the marks as one 64-bit mask per IP class (uint2 {tables 0-31, 32-63}), so a
-    // connection reads its two classes' masks once instead of one bitmap word per evaluation
+    // connection reads its two classes' masks once instead of one bitmap word per evaluation. Past
+    // 64 tables a bit covers a group of 2^gshift consecutive tables (bit t >> gshift): set when the
+    // class's row is the common one in every table of the group, so an evaluation whose group bit
+    // is clear gathers its entry from the cross table, which holds every row
+    uint32_t gshift = 0;
+    while (uni && (64u << gshift) < T) gshift++;
+    N.gshift = gshift;
     std::vector<uint32_t> masks(uni ? 2 * (size_t)G : 0, 0);
+    std::vector<uint8_t> grp_common(uni ? (size_t)G * 64 : 0, 1);  // [g][group]: every table common
     std::vector<uint32_t> crow(T, 0);
     for (uint32_t t : cov) {
-        const uint32_t base = img[N.tabinfo + 4 * t], nk = uni ? N.gk : an[t]->nkc;
+        const uint32_t base = TI[N.tabinfo + 4 * t], nk = uni ? N.gk : an[t]->nkc;
         // most frequent row: rows hashed, candidates compared word by word
         std::unordered_map<uint64_t, std::pair<uint32_t, uint32_t>> freq;  // hash -> (first ip class, count)
         auto row = [&](uint32_t g) { return X.data() + base + (size_t)g * nk; };
@@ -893,15 +901,19 @@ void build_common_rows(HostTableSet& h, const std::vector<uint32_t>& cov, const 
         }
         crow[t] = (uint32_t)sec.size();
         sec.insert(sec.end(), row(best), row(best) + nk);
-        for (uint32_t g = 0; g < G; g++)
-            if (std::equal(row(g), row(g) + nk, row(best))) {
-                if (uni) masks[2 * (size_t)g + (t >> 5)] |= 1u << (t & 31u);
-                else map[((size_t)t << rs) + (g >> 5)] |= 1u << (g & 31u);
-            }
+        for (uint32_t g = 0; g < G; g++) {
+            const bool same = std::equal(row(g), row(g) + nk, row(best));
+            if (uni && !same) grp_common[(size_t)g * 64 + (t >> gshift)] = 0;
+            if (!uni && same) map[((size_t)t << rs) + (g >> 5)] |= 1u << (g & 31u);
+        }
     }
+    if (uni)
+        for (uint32_t g = 0; g < G; g++)
+            for (uint32_t b = 0; b < 64 && (b << gshift) < T; b++)
+                if (grp_common[(size_t)g * 64 + b]) masks[2 * (size_t)g + (b >> 5)] |= 1u << (b & 31u);
     while (sec.size() % 4) sec.push_back(0);
     const uint32_t s0 = (uint32_t)img.size();
-    for (uint32_t t : cov) img[N.tabinfo + 4 * t + 2] = s0 + crow[t];
+    for (uint32_t t : cov) TI[N.tabinfo + 4 * t + 2] = s0 + crow[t];
     img.insert(img.end(), sec.begin(), sec.end());
     if (uni) {  // the masks live in the class records (words 2-3): class g's at word cmap + (g << 2)
         N.cmap = N.ipinfo + 2u;
@@ -920,6 +932,7 @@ void build_common_rows(HostTableSet& h, const std::vector<uint32_t>& cov, const 
 bool build_node(HostTableSet& h, const std::vector<TableAnalysis*>& an, const std::vector<NodePod>& pods,
                 const NodePod& node_end, const Tuning& tu) {
     h.node_img.clear();
+    h.node_aux.clear();
     h.node_cross.clear();
     h.node = DevNode{};
     h.node_rec_words = 0;
@@ -1079,7 +1092,8 @@ bool build_node(HostTableSet& h, const std::vector<TableAnalysis*>& an, const st
     bool has_lists = false;
     for (uint32_t t : cov)
         for (const auto& l : an[t]->clist) has_lists |= !l.empty();
-    const bool aligned = tu.node_uniform && C == T && PC == 0 && T <= 64 && pack_ok && (tu.node_list_table || !has_lists);
+    // (more than 64 tables: the common-row marks cover groups of 2^gshift tables, DevNode gshift)
+    const bool aligned = tu.node_uniform && C == T && PC == 0 && pack_ok && (tu.node_list_table || !has_lists);
     const int enc = aligned ? kEncNodeA : kEncNode;
     // IPv4 trie root: the smallest trie among the root strides that give the fewest levels (a
     // walk reads exactly depth words; a smaller image leaves LDS for the counter histogram --
@@ -1217,12 +1231,15 @@ bool build_node(HostTableSet& h, const std::vector<TableAnalysis*>& an, const st
         }
         while (img.size() % 4) img.push_back(0);
     }
-    N.tabinfo = (uint32_t)img.size();
-    img.resize(img.size() + 4 * (size_t)T, 0);
+    // (the uniform layout's kernels never read tabinfo and kmap: the builder keeps them off the
+    // image, in h.node_aux)
+    std::vector<uint32_t>& TI = uni ? h.node_aux : img;
+    N.tabinfo = (uint32_t)TI.size();
+    TI.resize(TI.size() + 4 * (size_t)T, 0);
     N.gk_shift = 0;
     while ((1u << N.gk_shift) < GK) N.gk_shift++;
-    N.kmap = (uint32_t)img.size();
-    img.resize(img.size() + (((size_t)T << N.gk_shift) + 1) / 2, 0);
+    N.kmap = (uint32_t)TI.size();
+    TI.resize(TI.size() + (((size_t)T << N.gk_shift) + 1) / 2, 0);
     while (img.size() % 4) img.push_back(0);
     // PAIR tables: per node IP class, the table's src class | dst class << 16
     std::vector<uint32_t> pmap_off(PC);
@@ -1252,18 +1269,18 @@ bool build_node(HostTableSet& h, const std::vector<TableAnalysis*>& an, const st
     for (size_t c = 0; c < C; c++) {
         const uint32_t t = cov[c];
         const TableAnalysis& A = *an[t];
-        img[N.tabinfo + 4 * t] = (uint32_t)X.size();
-        img[N.tabinfo + 4 * t + 1] = A.nkc | 0x80000000u;
+        TI[N.tabinfo + 4 * t] = (uint32_t)X.size();
+        TI[N.tabinfo + 4 * t + 1] = A.nkc | 0x80000000u;
         for (uint32_t g = 0; g < GK; g++) {
             const uint32_t ki = (t << N.gk_shift) + g;
-            img[N.kmap + ki / 2] |= kc_key[g][c] << ((ki & 1u) * 16u);
+            TI[N.kmap + ki / 2] |= kc_key[g][c] << ((ki & 1u) * 16u);
         }
         if (A.pair) {  // {pair map base, nkc | covered | PAIR, verdicts base, class map | ndc << 16}
-            img[N.tabinfo + 4 * t + 1] |= kNodePairFlag;
+            TI[N.tabinfo + 4 * t + 1] |= kNodePairFlag;
             X.insert(X.end(), A.pmap.begin(), A.pmap.end());
-            img[N.tabinfo + 4 * t + 2] = (uint32_t)X.size();
+            TI[N.tabinfo + 4 * t + 2] = (uint32_t)X.size();
             X.insert(X.end(), A.xv.begin(), A.xv.end());
-            img[N.tabinfo + 4 * t + 3] = pmap_off[q++] | (A.ndc << 16);
+            TI[N.tabinfo + 4 * t + 3] = pmap_off[q++] | (A.ndc << 16);
             continue;
         }
         std::vector<uint32_t> first(A.clist.empty() ? 0 : A.cverd.size(), 0xFFFFFFFFu);
@@ -1307,7 +1324,7 @@ bool build_node(HostTableSet& h, const std::vector<TableAnalysis*>& an, const st
     build_common_rows(h, xcov, an, tu, uni);
     N.uniform = uni;
     N.tstride = uni ? G * GK : 0;
-    N.crow0 = uni && N.cmap ? img[N.tabinfo + 2] : 0;  // table 0's common row: table t's at crow0 + t * GK
+    N.crow0 = uni && N.cmap ? TI[N.tabinfo + 2] : 0;  // table 0's common row: table t's at crow0 + t * GK
     X.resize(rec0, 0);
     X.insert(X.end(), recs.begin(), recs.end());
     // list-verdict table (DevNode lv0): list L's verdict for node IP class g at lv0 + L * G + g --
@@ -1359,7 +1376,7 @@ bool build_node(HostTableSet& h, const std::vector<TableAnalysis*>& an, const st
                      "node: T %u G %u GK %u uniform %u | ip root %u depth %u, key root %u depth %u | words: "
                      "ip trie %u, key trie %u, ip rec %u, key rec %u, tabinfo+kmap %u, common %u, lists %u, total %u\n",
                      T, N.n_ipc, N.gk, N.uniform, N.ip_s1, N.ip_depth, N.key_k1, N.key_depth, N.key_root,
-                     irec0 - N.key_root, krec0 - irec0, N.tabinfo - krec0, N.img_words_base - N.tabinfo,
+                     irec0 - N.key_root, krec0 - irec0, uni ? 0u : N.tabinfo - krec0, uni ? 0u : N.img_words_base - N.tabinfo,
                      (N.lrec ? N.lrec : N.img_words) - N.img_words_base, N.lrec ? N.img_words - N.lrec : 0,
                      N.img_words);
     return true;
