@@ -169,10 +169,11 @@ int pg_ctx_device(const pg_ctx* ctx);
  * no live rule of which tests dst, default 1), "fd" (1/0: fixed-depth form of dst-independent
  * cross-product tables, default 1), "node_common" (1/0: common-row section of node
  * images, default 1), "node_uniform" (1/0: the node's uniform cross layout where every table
- * is covered and none is in PAIR form, default 1), "node_list_table" (1/0: a node cross entry
- * whose table still has dst-specific rules ahead of its verdict resolves them by one read of a
- * list-verdict table indexed by the dst's node IP class -- the IPv4 classes then also separate
- * those rules' dst prefixes -- instead of walking dst records; default 1), "node_list_words"
+ * is covered and none is in PAIR form, default 1), "node_list_table" (1/0: in the uniform layout
+ * a node cross entry whose table still has dst-specific rules ahead of its verdict resolves them
+ * by one read of a list-verdict table indexed by the dst's node IP class -- the IPv4 classes then
+ * also separate those rules' dst prefixes -- instead of walking dst records; 0 = records, which
+ * rules the uniform layout out for a set with such rules; default 1), "node_list_words"
  * (record form: node dst records up to this many words go into the node image, so a launch that
  * stages the image walks them in LDS; default 4096, 0 = never), "pair" (1/0: the PAIR structure -- src x dst classes, then x key classes
  * -- for tables the cross product cannot take, default 1; 0 = candidate lists; 2 = wherever it

@@ -814,8 +814,9 @@ struct NodeEval {
             pos[j] = (w[j] & kNodeRecMask) << 2;
         }
         // list-verdict table (N.lv0): one read at [list][node IP class of the rule's dst-side
-        // address] (fastpath.cpp build_node; the only list form of the uniform layout)
-        if (UNI || N.lv0) {
+        // address] (fastpath.cpp build_node: the uniform layout's list form; the other layouts
+        // keep the records, so their kernels carry one list path only)
+        if constexpr (UNI) {
             const uint32_t(&cb)[Q] = rev ? cs : cd;
             PG_UNROLL
             for (int j = 0; j < Q; j++)

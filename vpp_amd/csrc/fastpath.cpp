@@ -948,14 +948,14 @@ bool build_node(HostTableSet& h, const std::vector<TableAnalysis*>& an, const st
     for (size_t c = 0; c < cov.size(); c++)
         if (an[cov[c]]->pair) pcov.push_back(c);
     // List tables (cross-product tables with dst-specific rules in front of some verdicts,
-    // clist): with Tuning::node_list_table the IPv4 partition also separates every address
+    // clist): with Tuning::node_list_table (uniform layout) the IPv4 partition also separates every address
     // range those rules' dst prefixes tell apart (the class key holds, per list table, which of
     // them contain the class), so a list resolves by the rule-dst-side address's class alone: one
     // entry of a list-verdict table [list][node IP class] instead of a walk over its records
     std::vector<size_t> lcov;  // indices into cov
     std::vector<std::vector<uint64_t>> lb;   // per list table: its dst interval starts
     std::vector<std::vector<uint32_t>> lcl;  // ... and their classes (set of containing prefixes)
-    if (tu.node_list_table)
+    if (tu.node_list_table && tu.node_uniform && cov.size() == T && pcov.empty())
         for (size_t c = 0; c < cov.size(); c++) {
             const TableAnalysis& A = *an[cov[c]];
             if (A.pair) continue;
@@ -1260,7 +1260,8 @@ bool build_node(HostTableSet& h, const std::vector<TableAnalysis*>& an, const st
     X.reserve(entries + 16);
     std::vector<uint32_t> recs;
     const size_t rec0 = (entries + 3) & ~(uint64_t)3;
-    const bool ltab = tu.node_list_table != 0;  // (every list table is in lcov then)
+    // the list-verdict table is the uniform layout's list form; the others keep the records
+    const bool ltab = uni && tu.node_list_table != 0;  // (every list table is in lcov then)
     struct ListRef {
         size_t c, e;  // the list of (covered table cov[c], src class x key class e)
     };
@@ -1333,7 +1334,7 @@ bool build_node(HostTableSet& h, const std::vector<TableAnalysis*>& an, const st
     N.lv0 = 0;
     h.node_list_tab_words = 0;
     if (!lists.empty()) {
-        if ((uint64_t)lists.size() * G > kNodeListTabBudget) {  // the record form instead (not uniform)
+        if ((uint64_t)lists.size() * G > kNodeListTabBudget) {  // the record form instead (so not uniform)
             Tuning t2 = tu;
             t2.node_list_table = 0;
             t2.node_uniform = 0;
