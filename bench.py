@@ -561,7 +561,9 @@ def cpu_baseline(w, b, out, k_max, faithful_s=8.0, budget_s=10.0):
         kind = "evalACL over the same ACL (rules pre-parsed)"
     else:
         wd = world.World(e, w.local_ifs, w.node_if)
-        sif, dif = wd.resolve(src), wd.resolve(dst)  # interface lookup kept outside the timed call
+        # interface lookup kept outside the timed call; CONN: the reference's Connection* end-point
+        # rules (no evaluation for remote pod <-> non-pod and non-pod <-> non-pod, World.conn_ifs)
+        sif, dif = wd.conn_ifs(src, dst) if w.mode == 2 else (None, wd.resolve(dst))
         if w.mode == 1:
             run = lambda k, th: fast.perpod(wd.acls, wd.if_out, dif[:k], src[:k], dst[:k], dport[:k], proto[:k], th)
             kind = "evalACL(outbound ACL of the dst interface), rules pre-parsed, interfaces resolved beforehand"

@@ -165,8 +165,11 @@ int pg_ctx_device(const pg_ctx* ctx);
  * "lc_dense12" (boundaries a subtree needs for a 12-bit stride, default 16), "lc_max_stride"
  * (widest level-compressed stride: 12, 16 or 18, default 16), "lc_root_bits" (src-trie root
  * stride cap of blobs read from HBM, whose root alone a launch stages in LDS: 4..14, default
- * 12), "candi" (1/0: candidates inline in the 8-B trie entries of HBM-resident candidate tables
- * no live rule of which tests dst, default 1), "fd" (1/0: fixed-depth form of dst-independent
+ * 13), "candi" (1/0: candidates inline in the 8-B trie entries of HBM-resident candidate tables
+ * no live rule of which tests dst, default 1), "candi_window_bits" (such a table's LDS window:
+ * the terminal entries of the 2^bits addresses of the aligned window where its earliest rules
+ * sit, staged with the root, so a lookup there makes no trie gather; 0..13, 0 = none, default
+ * 11; left out when it would not stage with the root), "fd" (1/0: fixed-depth form of dst-independent
  * cross-product tables, default 1), "node_common" (1/0: common-row section of node
  * images, default 1), "node_uniform" (1/0: the node's uniform cross layout where every table
  * is covered and none is in PAIR form, default 1), "node_list_table" (1/0: in the uniform layout

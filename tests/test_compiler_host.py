@@ -126,6 +126,55 @@ def test_candi_nested_prefixes_and_defaults(seed):
     check(e, "big", rules, tup)
 
 
+@pytest.mark.parametrize("wbits", [11, 8])
+def test_candi_window(wbits):
+    """CANDI window (fastpath.cpp, Tuning candi_window_bits): the terminal entries of the aligned
+    2^bits-address window where the earliest rules sit, staged with the root. Every address of
+    the window and past both of its edges, with classes of no candidate, one (inline) and several
+    (record list: nested lower-priority prefixes): the same verdicts as evalACL with and without
+    the window, and in the window no trie gather (an inline candidate reads LDS only)."""
+    rnd = random.Random(77)
+    rules, addr = [], 10 << 24
+    for k in range(6000):  # config 4's shape: disjoint /26../32 packed from 10.0.0.0 up
+        pl = rnd.randint(26, 32)
+        addr = (addr + (1 << (32 - pl)) - 1) & ~((1 << (32 - pl)) - 1)
+        r = {"action": rnd.randrange(2), "src": "%d.%d.%d.%d/%d" % (addr >> 24, addr >> 16 & 255, addr >> 8 & 255,
+                                                                     addr & 255, pl), "dst": ""}
+        addr += 1 << (32 - pl)
+        lo = rnd.randrange(1, 60000)
+        if k % 5 < 2:
+            r["tcp"] = {"src": [0, 65535], "dst": [lo, lo + rnd.choice([0, 10, 500])]}
+        elif k % 5 < 4:
+            r["udp"] = {"src": [0, 65535], "dst": [lo, lo + rnd.choice([0, 10, 500])]}
+        if k % 97 == 50:  # a hole: addresses no rule covers (the default, inline)
+            addr += 256
+        rules.append(r)
+    rules.insert(3000, {"action": 1, "src": "10.0.0.0/22", "dst": "", "tcp": {"src": [0, 65535], "dst": [0, 30000]}})
+    rules.insert(3001, {"action": 0, "src": "10.0.2.0/23", "dst": "", "udp": {"src": [0, 65535], "dst": [53, 53]}})
+    base, span = 10 << 24, 1 << wbits
+    n = 3 * span
+    src = (base - span + np.arange(n)).astype(np.uint32)  # the window and a window's width either side
+    g = np.random.default_rng(78)
+    proto = g.choice(np.array([0, 1, 2], np.uint8), n, p=[0.45, 0.45, 0.10])
+    dport = np.where(g.random(n) < 0.3, 53, g.integers(0, 65536, n)).astype(np.uint16)
+    tup = (src, g.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32), np.zeros(n, np.uint16), dport, proto)
+    gathers = {}
+    for wb in (wbits, 0):
+        with tuning("cross_max_rules", 0, 1 << 20), tuning("pair", 0, 1), tuning("candi_window_bits", wb, 11), \
+                tuning("lc_root_bits", 12, 13):  # (the root a window caps at 12 bits, both ways)
+            e = engine_with({"big": rules})
+            assert e.table_stats(0)["structure"] == "candi"
+        check(e, "big", rules, tup)
+        nl, nm, stage = e.debug_walk_stats(0, *tup[:2], tup[3], tup[4])
+        assert stage == 2
+        gathers[wb] = nm
+    inw = (src >= base) & (src < base + span)
+    assert (gathers[0] >= 1).all()  # no window: every lookup gathers
+    assert (gathers[wbits][~inw] == gathers[0][~inw]).all()
+    assert (gathers[wbits][inw] == 0).mean() > 0.3  # inline candidates and the default: LDS only
+    assert (gathers[wbits][inw] <= gathers[0][inw] - 1).all()
+
+
 def test_long_dst_lists_use_pair_mode():
     """global-table shape with long dst lists (egress to many pod /32s per port): PAIR mode,
     and the same verdicts with it disabled (cross product + dst lists)"""

@@ -37,6 +37,7 @@ constexpr uint32_t kFlagCandI = 128u;
 // first rule; kCandiDefault = the table's default verdict); w1 bit 31 set = kCandiInternal:
 // child block at word w0, stride w1 & 31; else the class's record list at record w0.
 constexpr uint32_t kCandiNode = 1u << 31, kCandiInternal = 1u << 30, kCandiDefault = 0x1FFFFFFu;
+
 constexpr uint32_t kPairHdr = 12u;  // PAIR blob header words: dst root, d1, pair table, n_dst_classes
 constexpr uint32_t kLeaf = 0x80000000u;
 // non-leaf trie entry: child block offset (words) | child stride << kTrieStrideShift
@@ -82,6 +83,16 @@ PG_HD constexpr uint32_t node_ip_rec_shift() { return A ? 4u : 2u; }
 template <bool A>
 PG_HD constexpr uint32_t node_key_rec_shift() { return A ? 5u : 2u; }
 constexpr uint32_t kSrcRoot = 16u;       // the src trie root follows the 16-word blob header
+// CANDI window (fastpath.cpp, the CANDI builder): blob words [candi_window_off, + 2 * size) after
+// the src root hold the terminal 8-B entry of every address of [base, base + size) (DevTable /
+// BlobTab kroot = base, nkc = size; size 0 = no window), staged in LDS with the root
+PG_HD constexpr uint32_t candi_window_off(uint32_t s1) { return kSrcRoot + (1u << s1); }
+// words of a blob's prefix a launch stages when the src root alone is staged: header, root and
+// (CANDI) the window, rounded to 16 B
+PG_HD constexpr uint32_t blob_root_words(uint32_t fsk, uint32_t nkc) {
+    return (((fsk & kFlagCandI) && nkc ? candi_window_off((fsk >> 8) & 0xFFu) + 2u * nkc
+                                       : kSrcRoot + (1u << ((fsk >> 8) & 0xFFu))) + 3u) & ~3u;
+}
 constexpr uint32_t kWalkKeyLimit = 0x30000u;  // keys >= this (ANY protocol) take the linear path
 // key bound of records that match every key: covers the whole 18-bit walk range, ANY keys
 // included, so every list terminates for any key the walk is given
@@ -125,19 +136,38 @@ PG_HD bool rec_match(const W4& r, uint32_t dst, uint32_t key) {
 // LDS copy, ld the blob in HBM; otherwise the same loaders).
 // CANDI lanes (ci) of a walk: the 4-B root (ld0), then 8-B entries until an inline candidate
 // (w set) or a pointer to the class's record list (pend, pos: the caller walks the records,
-// rec_walk). A lane that finished issues no further load.
+// rec_walk). A lane that finished issues no further load. An address in the table's window
+// reads its terminal entry from ld0 instead (no root read, no gather).
 template <class L, class L0, int Q>
 PG_HD void candi_walk(const L (&ld)[Q], const L0 (&ld0)[Q], const BlobTab (&tb)[Q], const bool (&ci)[Q],
                       const uint32_t (&src)[Q], const uint32_t (&key)[Q], uint32_t (&w)[Q], bool (&pend)[Q],
                       uint32_t (&pos)[Q]) {
     uint32_t cw[Q], cst[Q], ss[Q];
     bool cwalk[Q];
+    // a window entry (terminal): a record-list pointer or an inline candidate
+    auto entry = [&](int j, const W2& v) {
+        if (v.y & kCandiNode) {
+            pos[j] = tb[j].xoff + 4u * v.x;
+            pend[j] = true;
+            return;
+        }
+        const uint32_t klo = v.x & 0x3FFFFu, khi = (v.x >> 18) | ((v.y & 15u) << 14);
+        const uint32_t rel = (v.y >> 6) & kCandiDefault;
+        const bool hit = key[j] >= klo && key[j] <= khi && rel != kCandiDefault;
+        w[j] = hit ? (((v.y >> 4) & 3u) << 30) | (tb[j].rbase + rel) : tb[j].dflt;
+    };
     PG_UNROLL
     for (int j = 0; j < Q; j++) {
         cwalk[j] = false;
         cw[j] = cst[j] = ss[j] = 0;
         if (!ci[j]) continue;
-        ss[j] = 32u - ((tb[j].fsk >> 8) & 0xFFu);
+        const uint32_t s1 = (tb[j].fsk >> 8) & 0xFFu;
+        ss[j] = 32u - s1;
+        const uint32_t wd = src[j] - tb[j].kroot;
+        if (wd < tb[j].nkc) {  // the window: the address's terminal entry (never internal)
+            entry(j, ld0[j].u2(candi_window_off(s1) + 2u * wd));
+            continue;
+        }
         const uint32_t e = ld0[j].u32(kSrcRoot + (src[j] >> ss[j]));
         if (e & kLeaf) {
             pos[j] = tb[j].xoff + 4u * (e & ~kLeaf);
@@ -157,6 +187,8 @@ PG_HD void candi_walk(const L (&ld)[Q], const L0 (&ld0)[Q], const BlobTab (&tb)[
         for (int j = 0; j < Q; j++) {
             if (!cwalk[j]) continue;
             ss[j] -= cst[j];
+            // (the entry decoded in place, not through entry(): A/B on MI355X, config 4 with
+            // counters 108.8 vs 113.4 Gpps)
             const W2 v = ld[j].u2(cw[j] + 2u * ((src[j] >> ss[j]) & ((1u << cst[j]) - 1u)));
             if (v.y & kCandiNode) {
                 if (v.y & kCandiInternal) {

@@ -559,7 +559,7 @@ int pg_debug_walk_stats(pg_ctx* ctx, int table_id, const pg_tuple_soa* t, uint64
     const DevTable& hd = E.host.tabs[table_id];
     const Tuning& tu = E.tune;
     const uint32_t words = E.host.blob_words[table_id], prefix = E.host.blob_prefix[table_id];
-    const uint32_t root_words = (kSrcRoot + (1u << ((hd.fsk >> 8) & 0xFFu)) + 3u) & ~3u;
+    const uint32_t root_words = blob_root_words(hd.fsk, hd.nkc);
     const bool linear = (hd.fsk & kFlagLinear) != 0;
     // the launch device.hip launch_classify picks for this table (SINGLE mode)
     int st = 0;

@@ -1176,7 +1176,7 @@ static void launch_classify(const DevTableSet& T, const Tuning& tu, int t, const
     if constexpr (MODE == 0) {
         const DevTable& hd = T.host_tabs[t];
         const uint32_t words = T.host_blob_words[t];
-        const uint32_t root_words = (kSrcRoot + (1u << ((hd.fsk >> 8) & 0xFFu)) + 3u) & ~3u;
+        const uint32_t root_words = blob_root_words(hd.fsk, hd.nkc);  // (CANDI: + its window)
         const uint32_t prefix = T.host_blob_prefix[t];
         if ((hd.fsk & kFlagFD) && words <= tu.stage_max_words)  // FD blob in LDS, no dst stream
             launch_one<MODE, COUNT, VEC, 4, false>(T, tu, t, src, dst, sport, dport, proto, n, out, counters, st, hist,

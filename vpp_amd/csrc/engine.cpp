@@ -54,6 +54,7 @@ const Knob kKnobs[] = {
     {"node_common", &Tuning::node_common, 0, 1, true},
     {"fd", &Tuning::fd, 0, 1, true},
     {"candi", &Tuning::candi, 0, 1, true},
+    {"candi_window_bits", &Tuning::candi_window_bits, 0, 13, true},
     {"cross_max_rules", &Tuning::cross_max_rules, 0, 1 << 24, true},
     {"node_hist_cells", &Tuning::node_hist_cells, 0, 8192, false},
     {"node_list_words", &Tuning::node_list_words, 0, 16384, true},

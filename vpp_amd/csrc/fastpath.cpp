@@ -558,11 +558,21 @@ bool build_fast_table(const DevRule* rules, uint32_t n, uint32_t rule_base, uint
     // ends with its last trie read instead of a further record gather; on MI355X a gather costs
     // the same for 4 and 16 B, per active lane (tools/gather_probe.hip), so one gather less per
     // tuple is the lever for tables over LDS. Root leaves keep the record form.
+    // Window (Tuning::candi_window_bits, blobwalk.hpp candi_walk): right after the root, staged
+    // with it, the terminal 8-B entry of every address of one aligned 2^w-address window -- the
+    // window where the table's earliest rules sit (a first-match table's leading rules decide
+    // the most lookups: the reference's own scan cost is the matched rule's index) -- so a
+    // lookup there reads LDS only (an inline candidate) or goes straight to its record list.
     bool cand_dst_free = true;
     for (uint32_t i = 0; i < n; i++) cand_dst_free &= !live(rules[i]) || rules[i].dmask == 0;
     if (lc && tu.candi && cand_dst_free && n < kCandiDefault) {
         std::vector<uint32_t> tmp;  // the 4-B trie (kEncBlob, leaf = kLeaf | src class)
-        const uint32_t s1 = std::min<uint32_t>(pick_stride(sb.size(), 32, tu), tu.lc_root_bits);
+        // with a window the root takes at most 12 bits: header + root + a 2^11 window = 32 KiB, so
+        // four 512-thread workgroups still fit a CU's LDS (A/B on MI355X, config 4: 13-bit root
+        // without a window 190 Gpps, with a 2^10 window (three per CU) 176, 12-bit root + 2^11
+        // window 194)
+        const uint32_t s1 = std::min<uint32_t>(std::min<uint32_t>(pick_stride(sb.size(), 32, tu), tu.lc_root_bits),
+                                               tu.candi_window_bits ? 12u : 32u);
         if (build_trie(tmp, sb, sint_cls, 32, s1, tu, lc) == 0) {
             std::vector<int64_t> rec_of(nsc, -1);  // record list index of a class (root leaves, pointers)
             std::vector<uint32_t> rec_cls;
@@ -570,8 +580,23 @@ bool build_fast_table(const DevRule* rules, uint32_t n, uint32_t rule_base, uint
                 if (rec_of[c] < 0) rec_of[c] = (int64_t)rec_cls.size(), rec_cls.push_back(c);
                 return (uint32_t)rec_of[c];
             };
+            // the window: score 1 / (r + 1) per rule r whose src prefix fits in a window, summed
+            // per aligned window; the best one (the lower address on a tie), if it stages with the root
+            uint32_t wbase = 0, wsize = 0;
+            const uint32_t wb = tu.candi_window_bits;
+            if (wb && candi_window_off(s1) + (2ull << wb) <= tu.stage_root_max_words) {
+                std::map<uint32_t, double> score;
+                for (uint32_t r = 0; r < n && r < (1u << 16); r++) {
+                    const DevRule& R = rules[r];
+                    if (!live(R) || (uint32_t)__builtin_popcount(R.smask) < 32u - wb) continue;
+                    score[R.snet & ~((1u << wb) - 1u)] += 1.0 / (r + 1.0);
+                }
+                double best = 0;
+                for (const auto& kv : score)
+                    if (kv.second > best) best = kv.second, wbase = kv.first, wsize = 1u << wb;
+            }
             // blocks: (old offset, stride) -> new word offset; breadth-first from the root
-            blob.resize(kSrcRoot + (1u << s1), 0);
+            blob.resize(wsize ? candi_window_off(s1) + 2u * wsize : kSrcRoot + (1u << s1), 0);
             struct Blk {
                 uint32_t old_off, stride, new_off;
             };
@@ -621,10 +646,35 @@ bool build_fast_table(const DevRule* rules, uint32_t n, uint32_t rule_base, uint
                     blob[b.new_off + 2 * e + 1] = w1;
                 }
             }
+            // window entries: the address's src class (its elementary interval) -> its terminal
+            // entry (never internal), list numbers like the leaves' (turned into records below)
+            const uint32_t w0ff = candi_window_off(s1);
+            for (uint32_t d = 0; ok && d < wsize; d++) {
+                const uint64_t a = (uint64_t)wbase + d;
+                const size_t k = (size_t)(std::upper_bound(sb.begin(), sb.end(), a) - sb.begin()) - 1;
+                const uint32_t c = sint_cls[k];
+                const std::vector<uint32_t>& L = src_lists[c];
+                uint32_t w0, w1;
+                if (L.size() >= 2) {
+                    w0 = rec(c);
+                    w1 = kCandiNode;
+                } else if (L.empty()) {
+                    w0 = 0 | (kRecKeyAll & 0x3FFFu) << 18;
+                    w1 = (kRecKeyAll >> 14) | kCandiDefault << 6;
+                } else {
+                    const DevRule& R = rules[L[0]];
+                    w0 = R.klo | (R.khi & 0x3FFFu) << 18;
+                    w1 = (R.khi >> 14) | (R.act & 3u) << 4 | L[0] << 6;
+                }
+                blob[w0ff + 2 * d] = w0;
+                blob[w0ff + 2 * d + 1] = w1;
+            }
             if (ok) {
                 blob[0] = kFlagCandI;
                 blob[2] = kSrcRoot;
                 blob[3] = s1;
+                blob[4] = wbase;  // DevTable kroot / nkc: the window's first address and size (0: none)
+                blob[7] = wsize;
                 while (blob.size() % 4) blob.push_back(0);
                 blob[6] = (uint32_t)blob.size();
                 // record lists of the referenced classes, in reference order; rec(c) numbered the
@@ -644,6 +694,10 @@ bool build_fast_table(const DevRule* rules, uint32_t n, uint32_t rule_base, uint
                             uint32_t* v = &blob[q[qi].new_off + 2 * e];
                             if ((v[1] & kCandiNode) && !(v[1] & kCandiInternal)) v[0] = first[v[0]];
                         }
+                    for (uint32_t d = 0; d < wsize; d++) {
+                        uint32_t* v = &blob[w0ff + 2 * d];
+                        if (v[1] & kCandiNode) v[0] = first[v[0]];
+                    }
                     for (uint32_t c : rec_cls) {
                         const std::vector<uint32_t>& L = src_lists[c];
                         for (size_t i = 0; i < L.size(); i++) {
