@@ -169,7 +169,8 @@ int pg_ctx_device(const pg_ctx* ctx);
  * no live rule of which tests dst, default 1), "candi_window_bits" (such a table's LDS window:
  * the terminal entries of the 2^bits addresses of the aligned window where its earliest rules
  * sit, staged with the root, so a lookup there makes no trie gather; 0..13, 0 = none, default
- * 11; left out when it would not stage with the root), "fd" (1/0: fixed-depth form of dst-independent
+ * 11; left out when it would not stage with the root), "candi_window_root_bits" (root stride cap
+ * of a table with a window, default 12: root + window in 32 KiB), "fd" (1/0: fixed-depth form of dst-independent
  * cross-product tables, default 1), "node_common" (1/0: common-row section of node
  * images, default 1), "node_uniform" (1/0: the node's uniform cross layout where every table
  * is covered and none is in PAIR form, default 1), "node_list_table" (1/0: in the uniform layout

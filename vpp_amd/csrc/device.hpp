@@ -227,6 +227,7 @@ struct Tuning {
     uint32_t fd = 1;               // FD form of dst-independent CROSS tables that fit LDS
     uint32_t candi = 1;            // CANDI form (inline candidates) of dst-independent HBM-resident CAND tables
     uint32_t candi_window_bits = 11;  // CANDI: LDS window of 2^bits addresses' terminal entries (0 = none)
+    uint32_t candi_window_root_bits = 12;  // CANDI: root stride cap of a table with a window
     uint32_t cross_max_rules = 1u << 20;  // CROSS (cross product) considered up to this many rules (within budget)
     uint32_t node_hist_cells = 256;   // LDS slot-cache cells (rounded down to a power of two; < 16 = none)
                                       // of node launches whose set has more slots than the LDS histogram

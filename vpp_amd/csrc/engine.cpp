@@ -55,6 +55,7 @@ const Knob kKnobs[] = {
     {"fd", &Tuning::fd, 0, 1, true},
     {"candi", &Tuning::candi, 0, 1, true},
     {"candi_window_bits", &Tuning::candi_window_bits, 0, 13, true},
+    {"candi_window_root_bits", &Tuning::candi_window_root_bits, 4, 14, true},
     {"cross_max_rules", &Tuning::cross_max_rules, 0, 1 << 24, true},
     {"node_hist_cells", &Tuning::node_hist_cells, 0, 8192, false},
     {"node_list_words", &Tuning::node_list_words, 0, 16384, true},

@@ -567,12 +567,12 @@ bool build_fast_table(const DevRule* rules, uint32_t n, uint32_t rule_base, uint
     for (uint32_t i = 0; i < n; i++) cand_dst_free &= !live(rules[i]) || rules[i].dmask == 0;
     if (lc && tu.candi && cand_dst_free && n < kCandiDefault) {
         std::vector<uint32_t> tmp;  // the 4-B trie (kEncBlob, leaf = kLeaf | src class)
-        // with a window the root takes at most 12 bits: header + root + a 2^11 window = 32 KiB, so
+        // with a window the root takes at most candi_window_root_bits (12): header + root + a 2^11 window = 32 KiB, so
         // four 512-thread workgroups still fit a CU's LDS (A/B on MI355X, config 4: 13-bit root
         // without a window 190 Gpps, with a 2^10 window (three per CU) 176, 12-bit root + 2^11
         // window 194)
         const uint32_t s1 = std::min<uint32_t>(std::min<uint32_t>(pick_stride(sb.size(), 32, tu), tu.lc_root_bits),
-                                               tu.candi_window_bits ? 12u : 32u);
+                                               tu.candi_window_bits ? tu.candi_window_root_bits : 32u);
         if (build_trie(tmp, sb, sint_cls, 32, s1, tu, lc) == 0) {
             std::vector<int64_t> rec_of(nsc, -1);  // record list index of a class (root leaves, pointers)
             std::vector<uint32_t> rec_cls;
