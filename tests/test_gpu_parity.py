@@ -516,6 +516,50 @@ def test_large_table_root_staged_and_hbm_walks_equal_oracle():
     assert np.array_equal(outs[0], outs[1])
 
 
+def test_candi_window_edges_vs_oracle():
+    """CANDI window (Tuning candi_window_bits): config 4's table shape at 20k rules with nested
+    lower-priority prefixes in the window, every address of the window and a window's width either
+    side, walked by the launch that stages root + window (STAGE 6), with and without counters, and
+    with the window off: verdicts and hit counters equal evalACL's."""
+    rnd = random.Random(91)
+    rules, addr = [], 10 << 24
+    for k in range(20000):
+        pl = rnd.randint(26, 32)
+        addr = (addr + (1 << (32 - pl)) - 1) & ~((1 << (32 - pl)) - 1)
+        r = {"action": rnd.randrange(2), "src": "%d.%d.%d.%d/%d" % (addr >> 24, addr >> 16 & 255, addr >> 8 & 255,
+                                                                     addr & 255, pl), "dst": ""}
+        addr += 1 << (32 - pl)
+        lo = rnd.randrange(1, 60000)
+        if k % 5 < 2:
+            r["tcp"] = {"src": [0, 65535], "dst": [lo, lo + rnd.choice([0, 10, 500])]}
+        elif k % 5 < 4:
+            r["udp"] = {"src": [0, 65535], "dst": [lo, lo + rnd.choice([0, 10, 500])]}
+        if k % 97 == 50:
+            addr += 256
+        rules.append(r)
+    rules.insert(5000, {"action": 1, "src": "10.0.0.0/22", "dst": "", "tcp": {"src": [0, 65535], "dst": [0, 30000]}})
+    rules.insert(5001, {"action": 0, "src": "10.0.2.0/23", "dst": "", "udp": {"src": [0, 65535], "dst": [53, 53]}})
+    e = make_engine({"big": (None, rules)})
+    tid = e.table_id("out-big")
+    span, base = 1 << 11, 10 << 24
+    src = np.tile((base - span + np.arange(3 * span)).astype(np.uint32), 20)
+    n = len(src)
+    g = np.random.default_rng(92)
+    proto = g.choice(np.array([0, 1, 2, 7], np.uint8), n, p=[0.45, 0.44, 0.10, 0.01])
+    dport = np.where(g.random(n) < 0.3, 53, g.integers(0, 65536, n)).astype(np.uint16)
+    tup = (src, g.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32), np.zeros(n, np.uint16), dport, proto)
+    ea, es = expected_single(e, tid, rules, tup)
+    hist = np.bincount(es, minlength=e.num_counter_slots())
+    for wb in (11, 0):
+        e.set_tuning("candi_window_bits", wb)
+        assert e.table_stats(tid)["structure"] == "candi"
+        for counters in (False, True):
+            got, _ = run_single(e, tid, tup, counters=counters)
+            assert ((got >> 30) == ea).all() and ((got & 0x3FFFFFFF) == es).all(), (wb, counters)
+            if counters:
+                assert np.array_equal(D.read_counters(e), hist), wb
+
+
 @pytest.mark.parametrize("mode", [MODE_PERPOD, MODE_CONN])
 def test_large_node_set_counter_cache_vs_oracle(mode):
     """Config 6 (K8s objects -> 52 tables, 64.6k rules: more counter slots than the full LDS
