@@ -611,6 +611,101 @@ constexpr int kernel_wpe_max() {
 }
 // STAGE_ + 8 (SINGLE, STAGE 0-2): the table is dst-free (kFlagDstFree: no rule tests dst), so
 // the dst stream is not read
+// SINGLE over a CANDI table with root + window staged (STAGE 6), a group of P tuples per lane
+// at once, the walks compacted across the wave (PG_CANDI_COMPACT). A lookup the window resolves
+// (an inline candidate or the default) is done in LDS; every other walkable one -- a trie walk
+// from the root, or a window record list -- is numbered wave-wide (ballot + mbcnt per tuple
+// slot), its lane and slot written as one byte to the wave's 256-B LDS scratch, and the walks run
+// over the numbered lookups: lane i takes lookups r0 + i and r0 + 64 + i, pulling their address
+// and key from the owning lanes (ds_bpermute), then the owners pull the verdicts back. The wave
+// then issues its gathers for the lookups that need them only, in one lockstep pass of two per
+// lane for up to 128 of them, instead of P / 2 passes over every lane's every slot (the lanes the
+// window resolved only exec-masked). ANY-protocol packets take the linear scan on their lane.
+#ifndef PG_CANDI_COMPACT
+#define PG_CANDI_COMPACT 1
+#endif
+template <bool COUNT, int P>
+__device__ __forceinline__ void classify_candi_group(const DevTableSet& T, const DevTable& tab0, uint8_t* scr,
+                                                     const uint32_t (&s)[P], const uint32_t (&dp)[P],
+                                                     const uint32_t (&pr)[P], const Hist& h, uint32_t (&out)[P]) {
+#if defined(__HIP_DEVICE_COMPILE__)  // (device code only: wave intrinsics)
+    const uint32_t lane = __lane_id();
+    const LdsLoader l0{};
+    const DevLoader blob{T.blobs + tab0.blob_off};
+    const uint32_t wb = tab0.kroot, wsz = tab0.nkc, woff = candi_window_off((tab0.fsk >> 8) & 0xFFu);
+    uint32_t key[P], g[P];
+    bool pend[P];
+#pragma unroll
+    for (int j = 0; j < P; j++) {
+        key[j] = pkt_key(pr[j], dp[j]);
+        pend[j] = key[j] < kWalkKeyLimit;
+        out[j] = 0;
+        const uint32_t wd = s[j] - wb;
+        if (pend[j] && wd < wsz) {  // the window's terminal entry: an inline candidate or the default ends here
+            const W2 v = l0.u2(woff + 2u * wd);
+            if (!(v.y & kCandiNode)) {
+                const uint32_t klo = v.x & 0x3FFFFu, khi = (v.x >> 18) | ((v.y & 15u) << 14);
+                const uint32_t rel = (v.y >> 6) & kCandiDefault;
+                const bool hit = key[j] >= klo && key[j] <= khi && rel != kCandiDefault;
+                out[j] = hit ? (((v.y >> 4) & 3u) << 30) | (tab0.rule_base + rel) : tab0.dflt;
+                pend[j] = false;
+            }
+        }
+    }
+    uint32_t M = 0;  // walks left in the wave (uniform)
+#pragma unroll
+    for (int j = 0; j < P; j++) {
+        const unsigned long long m = __ballot(pend[j]);
+        g[j] = M + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+        if (pend[j]) scr[g[j]] = (uint8_t)(lane * 4u + (uint32_t)j);
+        M += (uint32_t)__popcll(m);
+    }
+    const BlobTab tb1{tab0.fsk, tab0.dflt, tab0.kroot, tab0.xoff, tab0.nkc, tab0.rule_base};
+    for (uint32_t r0 = 0; r0 < M; r0 += 128u) {
+        uint32_t vs[2], vk[2], res[2] = {0u, 0u}, pos[2] = {0u, 0u};
+        const uint32_t zero[2] = {0u, 0u};
+        bool on[2], pd[2] = {false, false};
+        const DevLoader ld[2] = {blob, blob};
+        const LdsLoader ld0[2] = {l0, l0};
+        const BlobTab tb[2] = {tb1, tb1};
+#pragma unroll
+        for (int q = 0; q < 2; q++) {
+            const uint32_t gi = r0 + 64u * (uint32_t)q + lane;
+            on[q] = gi < M;
+            const uint32_t id = on[q] ? (uint32_t)scr[gi] : 0u;
+            const int a = (int)((id >> 2) << 2);  // the owning lane, as a byte address
+            uint32_t xs = 0, xk = 0;
+#pragma unroll
+            for (int j = 0; j < P; j++) {
+                const uint32_t ps = (uint32_t)__builtin_amdgcn_ds_bpermute(a, (int)s[j]);
+                const uint32_t pk = (uint32_t)__builtin_amdgcn_ds_bpermute(a, (int)key[j]);
+                if ((id & 3u) == (uint32_t)j) xs = ps, xk = pk;
+            }
+            vs[q] = xs;
+            vk[q] = xk;
+        }
+        candi_walk(ld, ld0, tb, on, vs, vk, res, pd, pos);
+        rec_walk(ld, tb, zero, vk, pd, pos, res);
+#pragma unroll
+        for (int j = 0; j < P; j++) {  // the owners pull their verdicts back
+            const uint32_t rel = g[j] - r0;
+            const int a = (int)((rel & 63u) << 2);
+            const uint32_t v0 = (uint32_t)__builtin_amdgcn_ds_bpermute(a, (int)res[0]);
+            const uint32_t v1 = (uint32_t)__builtin_amdgcn_ds_bpermute(a, (int)res[1]);
+            if (pend[j] && rel < 128u) out[j] = rel < 64u ? v0 : v1;
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < P; j++)
+        if (key[j] >= kWalkKeyLimit)
+            out[j] = eval_linear(T.rules, tab0.rule_base, tab0.n_rules, tab0.dflt, s[j], 0u, key[j]);
+    if (COUNT) {
+#pragma unroll
+        for (int j = 0; j < P; j++) h.inc(out[j] & kSlotMask);
+    }
+#endif
+}
+
 template <int MODE, bool COUNT, bool VEC, int STAGE_, bool NODE, int BS>
 __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(kernel_wpe<MODE, COUNT, NODE, STAGE_>(),
                                                                     kernel_wpe_max<MODE, COUNT, NODE, STAGE_>())))
@@ -661,6 +756,9 @@ void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
     }
     // STAGE 2 / 6: only the header and src-trie root of a large blob are in LDS
     const uint32_t* rootb = (MODE == 0 && (STAGE == 2 || STAGE == 6)) ? smem : nullptr;
+    // STAGE 6 (PG_CANDI_COMPACT): each wave's 256-B scratch after the staged words and histogram
+    uint8_t* const cscr = reinterpret_cast<uint8_t*>(smem + stage_words + (COUNT ? hist_cells + 2u : 0u)) +
+                          (threadIdx.x >> 6) * 256u;
     // hit counters: an LDS histogram of the window [wbase, wbase + wn) of slots plus cells for
     // slots xslot and xslot1, flushed with one u64 atomic per non-zero cell; slots outside go to
     // global atomics. Every slot fits the window unless the table set has more than
@@ -787,6 +885,9 @@ void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
                                                         : (STAGE == 1   ? PG_QSINGLE_LDS
                                                            : STAGE == 6 ? (COUNT ? PG_QSINGLE : PG_QCANDI)
                                                                         : PG_QSINGLE)));
+        if constexpr (MODE == 0 && STAGE == 6 && PG_CANDI_COMPACT) {
+            classify_candi_group<COUNT, P>(T, tab0, cscr, sv, dpv, prv, h, o);
+        } else
 #pragma unroll
         for (int c = 0; c < P; c += QC) {
             uint32_t cs[QC], cd[QC], csp[QC], cdp[QC], cpr[QC], co[QC];
@@ -1079,7 +1180,8 @@ static void launch_bs(const DevTableSet& T, const Tuning& tu, int t, const uint3
     // the three LDS would allow (A/B on MI355X, config 2: 541-546 vs 533-535 Gpps, repeated
     // three times; with counters no difference): fewer streams in flight per CU contend less
     const uint32_t bpc = tu.blocks_per_cu ? tu.blocks_per_cu : (MODE == 0 && (STAGE & 7) == 4 && !COUNT ? 2u : 0u);
-    const size_t lds = hist + (size_t)stage * 4;
+    // (STAGE 6 with PG_CANDI_COMPACT: + 256 B of scratch per wave)
+    const size_t lds = hist + (size_t)stage * 4 + ((STAGE & 7) == 6 && PG_CANDI_COMPACT ? (size_t)BS * 4 : 0);
     // PERPOD / CONN over a uniform node: k_node_any after the classify kernel, for its deferred
     // ANY-protocol packets (PG_CONN_DEFER_ANY, PG_POD_DEFER_ANY; the launch's mark word and
     // number: dev_classify)
