@@ -662,7 +662,7 @@ PG_HD End node_end(const L& img, const DevNode& N, uint32_t ipc) {
     const uint32_t tin = v.y & 0xFFFFu, tout = v.y >> 16;
     return End{(int32_t)v.x, tin == 0xFFFFu ? -1 : (int32_t)tin, tout == 0xFFFFu ? -1 : (int32_t)tout};
 }
-// packed end point (uniform layout: at most 64 tables): interface index (14 bits) | end-point kind
+// packed end point (uniform layout: at most 254 tables): interface index (14 bits) | end-point kind
 // << 14 (0xFFFF: unresolved) | tin << 16 | tout << 24 (0xFF = no ACL)
 PG_HD End node_end_packed(uint32_t p) {
     const uint32_t f = p & 0xFFFFu, tin = (p >> 16) & 0xFFu, tout = p >> 24;
