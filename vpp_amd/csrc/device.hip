@@ -814,6 +814,7 @@ void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
     // lane (coalesced, non-temporal); prefetch 1/2: the next group's loads are in flight
     // while this group is classified
     constexpr int P = tuples_per_lane<MODE>();
+    static_assert(P % 4 == 0, "a group's protocol bytes are loaded as whole words (PG_TPL, PG_TPL_CONN)");
     const uint64_t nfull = VEC ? (n / P) : 0;
     struct Group {
         Words<P> s, d;
