@@ -567,12 +567,28 @@ bool build_fast_table(const DevRule* rules, uint32_t n, uint32_t rule_base, uint
     for (uint32_t i = 0; i < n; i++) cand_dst_free &= !live(rules[i]) || rules[i].dmask == 0;
     if (lc && tu.candi && cand_dst_free && n < kCandiDefault) {
         std::vector<uint32_t> tmp;  // the 4-B trie (kEncBlob, leaf = kLeaf | src class)
-        // with a window the root takes at most candi_window_root_bits (12): header + root + a 2^11 window = 32 KiB, so
-        // four 512-thread workgroups still fit a CU's LDS (A/B on MI355X, config 4: 13-bit root
-        // without a window 190 Gpps, with a 2^10 window (three per CU) 176, 12-bit root + 2^11
-        // window 194)
+        // the window: score 1 / (r + 1) per rule r whose src prefix fits in a window, summed per
+        // aligned window; the best one (the lower address on a tie)
+        uint32_t wbase = 0, wsize = 0;
+        const uint32_t wb = tu.candi_window_bits;
+        if (wb) {
+            std::map<uint32_t, double> score;
+            for (uint32_t r = 0; r < n && r < (1u << 16); r++) {
+                const DevRule& R = rules[r];
+                if (!live(R) || (uint32_t)__builtin_popcount(R.smask) < 32u - wb) continue;
+                score[R.snet & ~((1u << wb) - 1u)] += 1.0 / (r + 1.0);
+            }
+            double best = 0;
+            for (const auto& kv : score)
+                if (kv.second > best) best = kv.second, wbase = kv.first, wsize = 1u << wb;
+        }
+        // with a window the root takes at most candi_window_root_bits (12): header + root + a 2^11
+        // window = 32 KiB, so four 512-thread workgroups still fit a CU's LDS (A/B on MI355X,
+        // config 4: 13-bit root without a window 190 Gpps, with a 2^10 window (three per CU) 176,
+        // 12-bit root + 2^11 window 194); the window is left out when it does not stage with the root
         const uint32_t s1 = std::min<uint32_t>(std::min<uint32_t>(pick_stride(sb.size(), 32, tu), tu.lc_root_bits),
-                                               tu.candi_window_bits ? tu.candi_window_root_bits : 32u);
+                                               wsize ? tu.candi_window_root_bits : 32u);
+        if (wsize && candi_window_off(s1) + 2ull * wsize > tu.stage_root_max_words) wbase = wsize = 0;
         if (build_trie(tmp, sb, sint_cls, 32, s1, tu, lc) == 0) {
             std::vector<int64_t> rec_of(nsc, -1);  // record list index of a class (root leaves, pointers)
             std::vector<uint32_t> rec_cls;
@@ -580,21 +596,6 @@ bool build_fast_table(const DevRule* rules, uint32_t n, uint32_t rule_base, uint
                 if (rec_of[c] < 0) rec_of[c] = (int64_t)rec_cls.size(), rec_cls.push_back(c);
                 return (uint32_t)rec_of[c];
             };
-            // the window: score 1 / (r + 1) per rule r whose src prefix fits in a window, summed
-            // per aligned window; the best one (the lower address on a tie), if it stages with the root
-            uint32_t wbase = 0, wsize = 0;
-            const uint32_t wb = tu.candi_window_bits;
-            if (wb && candi_window_off(s1) + (2ull << wb) <= tu.stage_root_max_words) {
-                std::map<uint32_t, double> score;
-                for (uint32_t r = 0; r < n && r < (1u << 16); r++) {
-                    const DevRule& R = rules[r];
-                    if (!live(R) || (uint32_t)__builtin_popcount(R.smask) < 32u - wb) continue;
-                    score[R.snet & ~((1u << wb) - 1u)] += 1.0 / (r + 1.0);
-                }
-                double best = 0;
-                for (const auto& kv : score)
-                    if (kv.second > best) best = kv.second, wbase = kv.first, wsize = 1u << wb;
-            }
             // blocks: (old offset, stride) -> new word offset; breadth-first from the root
             blob.resize(wsize ? candi_window_off(s1) + 2u * wsize : kSrcRoot + (1u << s1), 0);
             struct Blk {
