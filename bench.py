@@ -55,8 +55,9 @@ def parse():
                    help="budget of the single-thread reference-faithful CPU variant")
     p.add_argument("--side", default="auto",
                    help="configs timed after the main line in labelled side blocks, same launches and "
-                        "self-check (comma list, 'none'; auto = 3 when the main config is 2 without "
-                        "--rules / --counters: the 10k-rule per-pod config north_star names)")
+                        "self-check (comma list, 'none'; auto = 3,4,5 when the main config is 2 without "
+                        "--rules / --counters: BASELINE.json configs[2..4] -- the 10k-rule per-pod config "
+                        "north_star names, the 100k-rule table, testConnection with hit counters)")
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--check-tuples", type=int, default=1 << 20,
                    help="tuples of every rank's shard checked against the oracle after the timed region")
@@ -215,13 +216,14 @@ def main():
         line["parity_per_rank"] = pars
     if rank == 0 and world == 1 and not a.no_cpu:
         line["cpu_baseline"] = cpu_baseline(w, b, out, a.cpu_sample, a.faithful_seconds, a.cpu_seconds)
-    side = a.side if a.side != "auto" else ("3" if a.config == 2 and not a.rules and not a.counters and
+    side = a.side if a.side != "auto" else ("3,4,5" if a.config == 2 and not a.rules and not a.counters and
                                              not a.tuples and not a.per_table else "none")
     if side != "none":
         del b, out, counters
         torch.cuda.empty_cache()
         for c in side.split(","):
             line["side_config%s" % c] = side_line(a, int(c), rank, world, local, launched, check_threads)
+            torch.cuda.empty_cache()
     if rank == 0:
         print(json.dumps(line), file=json_out, flush=True)
     if launched:
@@ -576,32 +578,41 @@ def cpu_baseline(w, b, out, k_max, faithful_s=8.0, budget_s=10.0):
     rate_1, k_1, _ = _timed_rate(lambda k: run(k, 1), k_max, budget_s / 2, 4096)
     got = out[:k_n].cpu().numpy().view(np.uint32)
     ok = bool(((got >> 30) == res[0].astype(np.uint32)).all() and ((got & 0x3FFFFFFF) == to_slot(res)).all())
-    if w.mode != 0:
-        # the reference-faithful variant of the same call: every evalACL parses its rules' CIDR
-        # strings on each rule visit (aclengine_mock.go:535, 549), one thread
-        if w.mode == 1:
-            frun = lambda k: fast.perpod(wd.acls, wd.if_out, dif[:k], src[:k], dst[:k], dport[:k], proto[:k],
-                                         faithful=True)
-        else:
-            frun = lambda k: fast.test_connection(wd.acls, wd.if_in, wd.if_out, sif[:k], dif[:k], src[:k], dst[:k],
-                                                  sport[:k], dport[:k], proto[:k], faithful=True)
-        fr, kf, fres = _timed_rate(frun, k_max, faithful_s, 4096)
-        extra["faithful_1thread_mpps"] = round(fr / 1e6, 4)
-        extra["faithful_sample"] = kf
-        extra["faithful_kind"] = kind.replace("rules pre-parsed", "CIDR strings parsed per rule visit") + ", 1 thread"
-        extra["faithful_variant_bit_exact"] = bool(((got[:kf] >> 30) == fres[0].astype(np.uint32)).all() and
-                                                   ((got[:kf] & 0x3FFFFFFF) == to_slot(fres)).all()) \
-            if kf <= k_n else None
+    # the reference-faithful variant of the same call: every evalACL parses its rules' CIDR strings
+    # on each rule visit (aclengine_mock.go:535, 549), at one thread and at every core (one engine
+    # per thread over a slice of the tuples: BASELINE.md B1, GOMAXPROCS=1 and GOMAXPROCS=$(nproc))
     if w.mode == 0:
         rules = e.GetACLByName(e.ACLNames()[w.table_id])["rules"]
-        fr, kf, (fa, fi) = _timed_rate(lambda k: fast.eval_acl_faithful(rules, src[:k], dst[:k], dport[:k], proto[:k]),
-                                       k_max, faithful_s, 64 if len(rules) > 20000 else 4096)
-        extra["faithful_1thread_mpps"] = round(fr / 1e6, 4)
-        extra["faithful_sample"] = kf
-        fslot = wd.slots(np.full(len(fi), t, np.int64), fi)
-        extra["faithful_variant_bit_exact"] = bool(((got[:kf] >> 30) == fa.astype(np.uint32)).all() and
-                                                   ((got[:kf] & 0x3FFFFFFF) == fslot[:kf]).all()) \
-            if kf <= k_n else None
+        frun = lambda k, th: fast.eval_acl_faithful(rules, src[:k], dst[:k], dport[:k], proto[:k], threads=th)
+        fslot = lambda r: wd.slots(np.full(len(r[1]), t, np.int64), r[1])
+        fcal = 64 if len(rules) > 20000 else 4096
+    else:
+        if w.mode == 1:
+            frun = lambda k, th: fast.perpod(wd.acls, wd.if_out, dif[:k], src[:k], dst[:k], dport[:k], proto[:k],
+                                             threads=th, faithful=True)
+        else:
+            frun = lambda k, th: fast.test_connection(wd.acls, wd.if_in, wd.if_out, sif[:k], dif[:k], src[:k],
+                                                      dst[:k], sport[:k], dport[:k], proto[:k], threads=th,
+                                                      faithful=True)
+        fslot = to_slot
+        fcal = 4096
+    fkind = kind.replace("rules pre-parsed", "CIDR strings parsed per rule visit")
+
+    def fcheck(k, r):  # (against the GPU's verdicts of the same k tuples)
+        g = out[:k].cpu().numpy().view(np.uint32)
+        return bool(((g >> 30) == r[0].astype(np.uint32)).all() and ((g & 0x3FFFFFFF) == fslot(r)).all())
+    fr, kf, fres = _timed_rate(lambda k: frun(k, 1), k_max, faithful_s, fcal)
+    extra["faithful_1thread_mpps"] = round(fr / 1e6, 4)
+    extra["faithful_sample"] = kf
+    extra["faithful_kind"] = fkind + ", 1 thread"
+    extra["faithful_variant_bit_exact"] = fcheck(kf, fres)
+    frn, kfn, fresn = _timed_rate(lambda k: frun(k, cores), k_max, faithful_s, fcal * cores)
+    extra["faithful_nthreads_mpps"] = round(frn / 1e6, 4)
+    extra["faithful_nthreads_cores"] = cores
+    extra["faithful_nthreads_sample"] = kfn
+    extra["faithful_nthreads_kind"] = fkind + ", %d threads (one engine per thread)" % cores
+    extra["faithful_nthreads_bit_exact"] = fcheck(kfn, fresn)
+    if w.mode == 0:
         idx = res[1]
         # rules the reference's first-match loop (aclengine_mock.go:510-649) visits per tuple
         nr = len(rules)

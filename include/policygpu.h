@@ -159,7 +159,9 @@ int pg_ctx_device(const pg_ctx* ctx);
  * -- "root_bits_max" (cap of the src/key trie root stride, 4..16, default 16), "node_build"
  * (1/0: build the node classifier for PERPOD / CONN, default 1), "node_root_bits" (its IPv4 /
  * key trie root stride cap, default 12), "node_key_root_bits" (cap of the uniform layout's
- * key trie root stride: 2, 6 or 10 bits -- 10 saves a level for ~4 KiB of image; default 8), "lc_lds" (table blobs of at least this many words are
+ * key trie root stride, 2..10; the strides tried are 2, 6 and 10 (18 - root a multiple of 4),
+ * so the cap is rounded down to one of them -- 10 saves a level for ~4 KiB of image; default
+ * 6), "lc_lds" (table blobs of at least this many words are
  * rebuilt with level-compressed 12/16-bit trie strides and keep them when the result still
  * fits in LDS; default 4096, 0 = off; blobs too large for LDS are always level-compressed),
  * "lc_dense12" (boundaries a subtree needs for a 12-bit stride, default 16), "lc_max_stride"
@@ -290,8 +292,9 @@ int pg_node_list_stats(pg_ctx* ctx, uint64_t* record_bytes, int* in_image);
  * array (0 = the record form, or no lists); PG_ENOENT: no node */
 int pg_node_list_table_stats(pg_ctx* ctx, uint64_t* table_bytes);
 /* 1 when the node classifier uses the uniform cross layout (every table covered, none in PAIR
- * form, tuning "node_uniform": entry addresses computed, no per-table info reads), else 0;
- * PG_ENOENT: no node */
+ * form, tuning "node_uniform": entry addresses computed, no per-table info reads), 2 when it does
+ * with wide class records (255 tables or more: 16-bit table ids, 32-bit common-row marks), else
+ * 0; PG_ENOENT: no node */
 int pg_node_uniform(pg_ctx* ctx);
 /* reference-shaped linear-scan kernel (K1) on one table, for validation and comparison */
 int pg_classify_linear(pg_ctx* ctx, int table_id, const pg_tuple_soa* tuples, uint64_t n, uint32_t* out,

@@ -24,15 +24,15 @@ def _load():
         subprocess.check_call(["make", "-s", "-C", os.path.dirname(_LIB) + "/.."])
     lib = C.CDLL(_LIB)
     P = C.c_void_p
-    lib.ora_eval_faithful.argtypes = [C.POINTER(ora_rule), C.c_int, P, P, P, P, C.c_size_t, P, P]
+    lib.ora_eval_faithful.argtypes = [C.POINTER(ora_rule), C.c_int, P, P, P, P, C.c_size_t, P, P, C.c_int]
     lib.ora_acl_new.restype = P
     lib.ora_acl_new.argtypes = [C.POINTER(ora_rule), C.c_int]
     lib.ora_acl_free.argtypes = [P]
     lib.ora_eval.argtypes = [P, P, P, P, P, C.c_size_t, P, P, C.c_int]
     lib.ora_conn.argtypes = [P, P, P, P, P, P, P, P, P, P, C.c_size_t, P, P, P, P, P, C.c_int]
     lib.ora_perpod.argtypes = [P, P, P, P, P, P, P, C.c_size_t, P, P, P, C.c_int]
-    lib.ora_conn_faithful.argtypes = [P, P, P, P, P, P, P, P, P, P, C.c_size_t, P, P, P]
-    lib.ora_perpod_faithful.argtypes = [P, P, P, P, P, P, P, C.c_size_t, P, P, P]
+    lib.ora_conn_faithful.argtypes = [P, P, P, P, P, P, P, P, P, P, C.c_size_t, P, P, P, C.c_int]
+    lib.ora_perpod_faithful.argtypes = [P, P, P, P, P, P, P, C.c_size_t, P, P, P, C.c_int]
     return lib
 
 
@@ -105,13 +105,16 @@ def eval_acl(acl, src, dst, dport, proto, threads=os.cpu_count() or 1):
     return act, idx
 
 
-def eval_acl_faithful(rules_dicts, src, dst, dport, proto):
+def eval_acl_faithful(rules_dicts, src, dst, dport, proto, threads=1):
+    """evalACL with the rules' CIDR strings parsed on every rule visit (aclengine_mock.go:535, 549),
+    one engine per thread over a slice of the tuples"""
     arr, keep = rules_from_dicts(rules_dicts)
     n = len(src)
     src, dst = np.ascontiguousarray(src, np.uint32), np.ascontiguousarray(dst, np.uint32)
     dport, proto = np.ascontiguousarray(dport, np.uint16), np.ascontiguousarray(proto, np.uint8)
     act, idx = np.empty(n, np.int32), np.empty(n, np.int32)
-    lib.ora_eval_faithful(arr, len(rules_dicts), _p(src), _p(dst), _p(dport), _p(proto), n, _p(act), _p(idx))
+    lib.ora_eval_faithful(arr, len(rules_dicts), _p(src), _p(dst), _p(dport), _p(proto), n, _p(act), _p(idx),
+                          threads)
     return act, idx
 
 
@@ -123,7 +126,7 @@ def test_connection(acls, if_in, if_out, sif, dif, src, dst, sport, dport, proto
     aclengine_mock.go:448-491 makes them: (tables int32[n, 4], indices int32[n, 4]), table -3 =
     no evaluation, -2 = the unresolved-interface FAILURE, -1 = no ACL (nil: PERMIT).
     faithful=True: every evalACL parses its rules' CIDR strings on each rule visit, as
-    aclengine_mock.go:535, 549 do (one thread; no trace)."""
+    aclengine_mock.go:535, 549 do (no trace; `threads` engines over slices of the tuples)."""
     n = len(src)
     harr = (C.c_void_p * max(1, len(acls)))(*[a.h for a in acls])
     cv = lambda a, dt: np.ascontiguousarray(a, dt)
@@ -134,7 +137,7 @@ def test_connection(acls, if_in, if_out, sif, dif, src, dst, sport, dport, proto
     if faithful:
         fa = _facls(acls)
         lib.ora_conn_faithful(C.cast(fa, C.c_void_p), _p(if_in), _p(if_out), _p(sif), _p(dif), _p(src), _p(dst),
-                              _p(sport), _p(dport), _p(proto), n, _p(conn), _p(lt), _p(li))
+                              _p(sport), _p(dport), _p(proto), n, _p(conn), _p(lt), _p(li), threads)
         return conn, lt, li
     evt = evi = None
     if trace:
@@ -150,7 +153,7 @@ def test_connection(acls, if_in, if_out, sif, dif, src, dst, sport, dport, proto
 def perpod(acls, if_out, dif, src, dst, dport, proto, threads=os.cpu_count() or 1, faithful=False):
     """evalACL(outbound ACL of the dst interface) per tuple. Returns (ACLAction, table
     (-1 = no ACL, -2 = unresolved interface), matched index (-1 = none)). faithful=True: CIDR
-    strings parsed on each rule visit (aclengine_mock.go:535, 549), one thread."""
+    strings parsed on each rule visit (aclengine_mock.go:535, 549)."""
     n = len(src)
     harr = (C.c_void_p * max(1, len(acls)))(*[a.h for a in acls])
     cv = lambda a, dt: np.ascontiguousarray(a, dt)
@@ -160,7 +163,7 @@ def perpod(acls, if_out, dif, src, dst, dport, proto, threads=os.cpu_count() or 
     if faithful:
         fa = _facls(acls)
         lib.ora_perpod_faithful(C.cast(fa, C.c_void_p), _p(if_out), _p(dif), _p(src), _p(dst), _p(dport), _p(proto),
-                                n, _p(act), _p(lt), _p(li))
+                                n, _p(act), _p(lt), _p(li), threads)
         return act, lt, li
     lib.ora_perpod(C.cast(harr, C.c_void_p), _p(if_out), _p(dif), _p(src), _p(dst), _p(dport), _p(proto), n,
                    _p(act), _p(lt), _p(li), threads)

@@ -211,10 +211,43 @@ static int eval_faithful_one(const ora_rule* R, int n, uint32_t src, uint32_t ds
     return A_DENY;
 }
 
+/* Threads of the faithful variants: one engine per thread over a contiguous slice of the tuples,
+ * as BASELINE.md's B1 row runs the Go classifier with one engine per goroutine at
+ * GOMAXPROCS=1 and GOMAXPROCS=$(nproc). Nothing is shared but the read-only rule strings. */
+typedef struct {
+    const ora_rule* rules;
+    int n_rules;
+    const uint32_t *src, *dst;
+    const uint16_t* dport;
+    const uint8_t* proto;
+    int32_t *act, *idx;
+    size_t lo, hi;
+} faithful_job;
+
+static void* faithful_worker(void* p) {
+    faithful_job* j = (faithful_job*)p;
+    for (size_t i = j->lo; i < j->hi; i++)
+        j->act[i] = eval_faithful_one(j->rules, j->n_rules, j->src[i], j->dst[i], j->proto[i], j->dport[i], &j->idx[i]);
+    return NULL;
+}
+
 int ora_eval_faithful(const ora_rule* rules, int n_rules, const uint32_t* src, const uint32_t* dst,
-                      const uint16_t* dport, const uint8_t* proto, size_t n, int32_t* out_action, int32_t* out_idx) {
-    for (size_t i = 0; i < n; i++)
-        out_action[i] = eval_faithful_one(rules, n_rules, src[i], dst[i], proto[i], dport[i], &out_idx[i]);
+                      const uint16_t* dport, const uint8_t* proto, size_t n, int32_t* out_action, int32_t* out_idx,
+                      int threads) {
+    if (threads < 1) threads = 1;
+    if (threads > 256) threads = 256;
+    pthread_t th[256];
+    faithful_job jobs[256];
+    size_t per = (n + threads - 1) / threads;
+    for (int t = 0; t < threads; t++) {
+        size_t lo = t * per, hi = (t + 1) * per < n ? (t + 1) * per : n;
+        if (lo > hi) lo = hi;
+        jobs[t] = (faithful_job){rules, n_rules, src, dst, dport, proto, out_action, out_idx, lo, hi};
+        if (threads == 1) faithful_worker(&jobs[t]);
+        else pthread_create(&th[t], NULL, faithful_worker, &jobs[t]);
+    }
+    if (threads > 1)
+        for (int t = 0; t < threads; t++) pthread_join(th[t], NULL);
     return 0;
 }
 
@@ -469,22 +502,49 @@ int ora_perpod(const ora_acl* const* acls, const int32_t* if_out, const int32_t*
 
 /* ---------------- the same, reference-faithful: CIDR strings parsed on every rule visit ----------
  * (evalACL as aclengine_mock.go:535, 549 runs it: net.ParseCIDR per rule per packet), over the raw
- * rules of every table; single-threaded by intent (the reference-shaped CPU baseline). */
+ * rules of every table; at one thread and at every core (one engine per thread over a slice of the
+ * tuples: BASELINE.md B1, GOMAXPROCS=1 and GOMAXPROCS=$(nproc)). */
+static void run_jobs(conn_job* jobs, int threads, void* (*worker)(void*)) {
+    pthread_t th[256];
+    if (threads == 1) {
+        worker(&jobs[0]);
+        return;
+    }
+    for (int t = 0; t < threads; t++) pthread_create(&th[t], NULL, worker, &jobs[t]);
+    for (int t = 0; t < threads; t++) pthread_join(th[t], NULL);
+}
+
 int ora_conn_faithful(const ora_facl* facls, const int32_t* if_in, const int32_t* if_out, const int32_t* sif,
                       const int32_t* dif, const uint32_t* src, const uint32_t* dst, const uint16_t* sport,
                       const uint16_t* dport, const uint8_t* proto, size_t n, int32_t* out_conn,
-                      int32_t* out_last_table, int32_t* out_last_idx) {
-    conn_job j = {NULL, if_in, if_out, sif, dif, src, dst, sport, dport, proto, out_conn, out_last_table,
-                  out_last_idx, NULL, NULL, 0, n, facls};
-    conn_worker(&j);
+                      int32_t* out_last_table, int32_t* out_last_idx, int threads) {
+    if (threads < 1) threads = 1;
+    if (threads > 256) threads = 256;
+    conn_job jobs[256];
+    size_t per = (n + threads - 1) / threads;
+    for (int t = 0; t < threads; t++) {
+        size_t lo = t * per, hi = (t + 1) * per < n ? (t + 1) * per : n;
+        if (lo > hi) lo = hi;
+        jobs[t] = (conn_job){NULL, if_in, if_out, sif, dif, src, dst, sport, dport, proto, out_conn, out_last_table,
+                             out_last_idx, NULL, NULL, lo, hi, facls};
+    }
+    run_jobs(jobs, threads, conn_worker);
     return 0;
 }
 
 int ora_perpod_faithful(const ora_facl* facls, const int32_t* if_out, const int32_t* dif, const uint32_t* src,
                         const uint32_t* dst, const uint16_t* dport, const uint8_t* proto, size_t n,
-                        int32_t* out_action, int32_t* out_table, int32_t* out_idx) {
-    conn_job j = {NULL, NULL, if_out, NULL, dif, src, dst, NULL, dport, proto, out_action, out_table, out_idx,
-                  NULL, NULL, 0, n, facls};
-    perpod_worker(&j);
+                        int32_t* out_action, int32_t* out_table, int32_t* out_idx, int threads) {
+    if (threads < 1) threads = 1;
+    if (threads > 256) threads = 256;
+    conn_job jobs[256];
+    size_t per = (n + threads - 1) / threads;
+    for (int t = 0; t < threads; t++) {
+        size_t lo = t * per, hi = (t + 1) * per < n ? (t + 1) * per : n;
+        if (lo > hi) lo = hi;
+        jobs[t] = (conn_job){NULL, NULL, if_out, NULL, dif, src, dst, NULL, dport, proto, out_action, out_table,
+                             out_idx, NULL, NULL, lo, hi, facls};
+    }
+    run_jobs(jobs, threads, perpod_worker);
     return 0;
 }

@@ -41,10 +41,14 @@ def test_conn_baseline_uses_the_connection_endpoint_rules():
     r = _run(w, 1 << 14)
     assert r["sample_bit_exact_vs_gpu"] is True
     assert r["faithful_variant_bit_exact"] is True
+    assert r["faithful_nthreads_bit_exact"] is True and r["faithful_nthreads_cores"] == bench.host_cores()
 
 
 def test_perpod_baseline_bit_exact():
+    """PERPOD (config 3): the pre-parsed and the reference-faithful samples, at one thread and at
+    every core, equal the product's verdicts."""
     w = W.config3(0, n_tuples=1 << 14)
     r = _run(w, 1 << 14)
     assert r["sample_bit_exact_vs_gpu"] is True
     assert r["faithful_variant_bit_exact"] is True
+    assert r["faithful_nthreads_bit_exact"] is True and r["faithful_nthreads_cores"] == bench.host_cores()

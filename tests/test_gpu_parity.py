@@ -271,21 +271,24 @@ def test_generator_matches_numpy_restatement():
             assert np.array_equal(np.asarray(g), np.asarray(x))
 
 
-@pytest.mark.parametrize("config,mode", [(3, None), (5, None), (8, None), (8, MODE_CONN)],
-                         ids=["3", "5", "8", "8conn"])
+@pytest.mark.parametrize("config,mode", [(3, None), (5, None), (8, None), (8, MODE_CONN), (9, None), (9, MODE_CONN)],
+                         ids=["3", "5", "8", "8conn", "9", "9conn"])
 def test_cluster_configs_gpu_vs_oracle(config, mode):
-    """Configs 3 (PERPOD) and 5 (CONN) at full topology (1k pods, ~10k rules), and config 8 --
-    the same cluster with 20 apps per namespace: 202 per-pod tables, past the 64 one common-row
-    mask bit each covers (grouped marks) -- in both modes; 2M device-generated tuples, with hit
-    counters, bit-exact against the C oracle through oracle.world."""
+    """Configs 3 (PERPOD) and 5 (CONN) at full topology (1k pods, ~10k rules), config 8 -- the
+    same cluster with 20 apps per namespace: 202 per-pod tables, past the 64 one common-row mask
+    bit each covers (grouped marks) -- and config 9 -- 50 apps per namespace: 502 tables, past
+    the 254 whose ids fit a byte of a class record (wide records) -- in both modes; 2M
+    device-generated tuples, with hit counters (and the uncounted launch), bit-exact against the
+    C oracle through oracle.world."""
     from oracle.world import World
     from vpp_amd import workloads as W
     w = W.CONFIGS[config](0, n_tuples=2 << 20)
     e = w.engine
     mode = w.mode if mode is None else mode
-    if config == 8:
+    if config in (8, 9):
         ns = e.node_stats()
         assert e.num_tables() > 64 and ns["uniform"] and ns["common_row_pairs"] > 0.5 * ns["table_ipclass_pairs"], ns
+        assert ns["wide_records"] == (config == 9), ns
     b = D.TupleBatch(w.n_tuples, with_sport=(mode == MODE_CONN))
     D.gen_tuples(e, b, **w.gen)
     out = torch.empty(b.n, dtype=torch.int32, device="cuda")
@@ -309,6 +312,9 @@ def test_cluster_configs_gpu_vs_oracle(config, mode):
     assert ((got >> 30) == act.astype(np.uint32)).all()
     assert ((got & 0x3FFFFFFF) == slot).all()
     assert len(np.unique(got >> 30)) >= 2
+    D.classify(e, mode, -1, b, out)  # the launch without counters: the same verdicts
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy().view(np.uint32), got)
 
 
 @pytest.mark.parametrize("any_pct", [0.05, 1.0])
@@ -516,11 +522,14 @@ def test_large_table_root_staged_and_hbm_walks_equal_oracle():
     assert np.array_equal(outs[0], outs[1])
 
 
-def test_candi_window_edges_vs_oracle():
+@pytest.mark.parametrize("n_tuples", [122880, 122917, 200003])
+def test_candi_window_edges_vs_oracle(n_tuples):
     """CANDI window (Tuning candi_window_bits): config 4's table shape at 20k rules with nested
     lower-priority prefixes in the window, every address of the window and a window's width either
     side, walked by the launch that stages root + window (STAGE 6), with and without counters, and
-    with the window off: verdicts and hit counters equal evalACL's."""
+    with the window off: verdicts and hit counters equal evalACL's. Batch sizes: a multiple of
+    64 lanes x 4 tuples, and two that are not (the last wave of the grid-stride loop then runs
+    with only its first lanes active: the compacted walks must go to those lanes only)."""
     rnd = random.Random(91)
     rules, addr = [], 10 << 24
     for k in range(20000):
@@ -542,7 +551,7 @@ def test_candi_window_edges_vs_oracle():
     e = make_engine({"big": (None, rules)})
     tid = e.table_id("out-big")
     span, base = 1 << 11, 10 << 24
-    src = np.tile((base - span + np.arange(3 * span)).astype(np.uint32), 20)
+    src = np.tile((base - span + np.arange(3 * span)).astype(np.uint32), -(-n_tuples // (3 * span)))[:n_tuples]
     n = len(src)
     g = np.random.default_rng(92)
     proto = g.choice(np.array([0, 1, 2, 7], np.uint8), n, p=[0.45, 0.44, 0.10, 0.01])

@@ -209,6 +209,32 @@ def test_config8_more_than_64_tables_uniform_grouped_marks():
     assert np.array_equal(got0, got)
 
 
+def test_config9_more_than_254_tables_wide_records():
+    """Config 9 (config 3's cluster with 50 apps per namespace: 502 per-pod tables, past the 254
+    whose ids fit a byte of the class record): still the uniform layout, with wide class records
+    (16-bit table ids beside 32-bit grouped common-row marks), and PERPOD / CONN with counters
+    equal the oracle, the per-table path and the layout without common rows."""
+    w = W.config9(0, n_tuples=1 << 16)
+    e = w.engine
+    ns = e.node_stats()
+    assert e.num_tables() > 254 and ns["uniform"] and ns["wide_records"] and ns["image_bytes"] <= 64 << 10, ns
+    assert ns["common_row_pairs"] >= 0.5 * ns["table_ipclass_pairs"], ns
+    src, dst, sport, dport, proto = gen.gen_tuples(40001, **w.gen)
+    wd = World(e, w.local_ifs, w.node_if)
+    act, slot = wd.perpod(src, dst, dport, proto, threads=8)
+    got, cnt = e.debug_classify_host(MODE_PERPOD, -1, src, dst, sport, dport, proto, node=True, counters=True)
+    assert np.array_equal(got >> 30, act.astype(np.uint32)) and np.array_equal(got & 0x3FFFFFFF, slot)
+    assert np.array_equal(cnt, np.bincount(got & 0x3FFFFFFF, minlength=len(cnt)))
+    assert np.array_equal(e.debug_classify_host(MODE_PERPOD, -1, src, dst, sport, dport, proto, node=False), got)
+    conn, cslot, hist = wd.conn(src, dst, sport, dport, proto, threads=8, hist=True)
+    got, cnt = e.debug_classify_host(MODE_CONN, -1, src, dst, sport, dport, proto, node=True, counters=True)
+    assert np.array_equal(got >> 30, conn.astype(np.uint32)) and np.array_equal(got & 0x3FFFFFFF, cslot)
+    assert np.array_equal(cnt, hist)
+    got0 = e.debug_classify_host(MODE_CONN, -1, src, dst, sport, dport, proto, node=True, common=False)
+    assert np.array_equal(got0, got)
+    assert len(set((got >> 30).tolist())) >= 3
+
+
 def test_node_lists_table_or_records_in_image_or_cross():
     """A node cross entry with dst-specific rules ahead of its verdict resolves them the same
     three ways, all equal to the oracle: by the list-verdict table (default: one read at [list]
@@ -241,6 +267,49 @@ def test_node_lists_table_or_records_in_image_or_cross():
     act, slot = wd.perpod(src, dst, dport, proto, threads=8)
     assert np.array_equal(a >> 30, act.astype(np.uint32)) and np.array_equal(a & 0x3FFFFFFF, slot)
     conn, cslot = wd.conn(src, dst, sport, dport, proto, threads=8)
+    assert np.array_equal(c >> 30, conn.astype(np.uint32)) and np.array_equal(c & 0x3FFFFFFF, cslot)
+
+
+def test_list_table_at_dst_prefix_edges():
+    """The list-verdict table answers a list by the node IP class of the rule's dst-side address,
+    built from one address per class; that holds only if every address of a class lies in the
+    same dst prefixes of every list table (the class key). Checked where it would break first:
+    the first and last address of every dst prefix of every table, and their neighbours, as dst
+    (PERPOD, CONN SYN) and as src (CONN SYN-ACK), against the record form (node_list_table=0)
+    and the oracle."""
+    import ipaddress
+    w = W.config3(0, n_tuples=1 << 10, n_ns=4)
+    e = w.engine
+    assert e.node_stats()["list_table_bytes"] > 0
+    edges = set()
+    for name in e.ACLNames():
+        for r in e.GetACLByName(name)["rules"]:
+            if r.get("dst"):
+                net = ipaddress.ip_network(r["dst"], strict=False)
+                lo, hi = int(net.network_address), int(net.broadcast_address)
+                edges.update(x & 0xFFFFFFFF for x in (lo - 1, lo, lo + 1, hi - 1, hi, hi + 1))
+    edges = np.array(sorted(edges), np.uint32)
+    rng = np.random.default_rng(5)
+    pods = np.array(list(w.local_ifs), np.uint32)
+    n = 20 * len(edges)
+    dst = np.tile(edges, 20)
+    src = pods[rng.integers(0, len(pods), n)]
+    swap = rng.random(n) < 0.5  # the edge address as src too (CONN's reverse evaluations)
+    src[swap], dst[swap] = dst[swap], src[swap]
+    proto = rng.choice(np.array([0, 1], np.uint8), n)
+    dport = np.array(W.CLUSTER_PORTS, np.uint16)[rng.integers(0, len(W.CLUSTER_PORTS), n)]
+    sport = np.array(W.CLUSTER_PORTS, np.uint16)[rng.integers(0, len(W.CLUSTER_PORTS), n)]
+    tup = (src, dst, sport, dport, proto)
+    a = e.debug_classify_host(MODE_PERPOD, -1, *tup, node=True)
+    c = e.debug_classify_host(MODE_CONN, -1, *tup, node=True)
+    with e.tuning(node_list_table=0):
+        assert e.node_stats()["list_table_bytes"] == 0
+        assert np.array_equal(e.debug_classify_host(MODE_PERPOD, -1, *tup, node=True), a)
+        assert np.array_equal(e.debug_classify_host(MODE_CONN, -1, *tup, node=True), c)
+    wd = World(e, w.local_ifs, w.node_if)
+    act, slot = wd.perpod(src, dst, dport, proto, threads=8)
+    assert np.array_equal(a >> 30, act.astype(np.uint32)) and np.array_equal(a & 0x3FFFFFFF, slot)
+    conn, cslot = wd.conn(*tup, threads=8)
     assert np.array_equal(c >> 30, conn.astype(np.uint32)) and np.array_equal(c & 0x3FFFFFFF, cslot)
 
 

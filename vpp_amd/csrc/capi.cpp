@@ -636,7 +636,7 @@ DevTableSet host_view(const HostTableSet& h) {
     return v;
 }
 
-template <int MODE, int Q, bool PRED, bool CM, bool UNI>
+template <int MODE, int Q, bool PRED, bool CM, bool UNI, bool WIDE>
 void host_q(const DevTableSet& T, bool node, int table_id, const pg_tuple_soa* t, uint64_t i, uint32_t* out,
             const Hist& h) {
     uint32_t s[Q], d[Q], sp[Q], dp[Q], pr[Q], o[Q];
@@ -653,26 +653,28 @@ void host_q(const DevTableSet& T, bool node, int table_id, const pg_tuple_soa* t
             classify_q<0, true, Q, PRED>(T, T.blobs, tab, s, d, sp, dp, pr, h, o);
         }
     } else {
-        if (node) classify_node_q<MODE, true, Q, PRED, CM, false, UNI>(T, T.node, DevLoader{T.node.img}, s, d, sp, dp, pr, h, o);
+        if (node)
+            classify_node_q<MODE, true, Q, PRED, CM, false, UNI, false, WIDE>(T, T.node, DevLoader{T.node.img}, s, d, sp, dp,
+                                                                          pr, h, o);
         else classify_q<MODE, true, Q, PRED>(T, T.blobs, DevTable{}, s, d, sp, dp, pr, h, o);
     }
     for (int j = 0; j < Q; j++) out[i + j] = o[j];
 }
 
-template <int MODE, bool PRED, bool CM, bool UNI>
+template <int MODE, bool PRED, bool CM, bool UNI, bool WIDE>
 void host_classify(const DevTableSet& T, bool node, int table_id, const pg_tuple_soa* t, uint64_t n, uint32_t* out,
                    const Hist& h) {
     const uint64_t nq = n & ~(uint64_t)3;  // the kernels' quads, then one tuple at a time
-    for (uint64_t i = 0; i < nq; i += 4) host_q<MODE, 4, PRED, CM, UNI>(T, node, table_id, t, i, out, h);
-    for (uint64_t i = nq; i < n; i++) host_q<MODE, 1, PRED, CM, UNI>(T, node, table_id, t, i, out, h);
+    for (uint64_t i = 0; i < nq; i += 4) host_q<MODE, 4, PRED, CM, UNI, WIDE>(T, node, table_id, t, i, out, h);
+    for (uint64_t i = nq; i < n; i++) host_q<MODE, 1, PRED, CM, UNI, WIDE>(T, node, table_id, t, i, out, h);
 }
-template <int MODE, bool UNI>
+template <int MODE, bool UNI, bool WIDE = false>
 void host_classify(const DevTableSet& T, bool node, bool pred, bool cm, int table_id, const pg_tuple_soa* t,
                    uint64_t n, uint32_t* out, const Hist& h) {
-    if (pred && cm) host_classify<MODE, true, true, UNI>(T, node, table_id, t, n, out, h);
-    else if (pred) host_classify<MODE, true, false, UNI>(T, node, table_id, t, n, out, h);
-    else if (cm) host_classify<MODE, false, true, UNI>(T, node, table_id, t, n, out, h);
-    else host_classify<MODE, false, false, UNI>(T, node, table_id, t, n, out, h);
+    if (pred && cm) host_classify<MODE, true, true, UNI, WIDE>(T, node, table_id, t, n, out, h);
+    else if (pred) host_classify<MODE, true, false, UNI, WIDE>(T, node, table_id, t, n, out, h);
+    else if (cm) host_classify<MODE, false, true, UNI, WIDE>(T, node, table_id, t, n, out, h);
+    else host_classify<MODE, false, false, UNI, WIDE>(T, node, table_id, t, n, out, h);
 }
 }  // namespace
 
@@ -694,9 +696,12 @@ int pg_debug_classify_host(pg_ctx* ctx, int mode, int table_id, const pg_tuple_s
     const bool cm = use_node && (node & 4) && T.node.cmap != 0;
     const Hist h{nullptr, (unsigned long long*)counters};
     const bool uni = use_node && T.node.uniform;  // the layout the node was built with
+    const bool wide = uni && T.node.wide;          // ... and its class records
     if (mode == 0) host_classify<0, false>(T, false, pred, false, table_id, t, n, out, h);
+    else if (mode == 1 && wide) host_classify<1, true, true>(T, use_node, pred, cm, table_id, t, n, out, h);
     else if (mode == 1 && uni) host_classify<1, true>(T, use_node, pred, cm, table_id, t, n, out, h);
     else if (mode == 1) host_classify<1, false>(T, use_node, pred, cm, table_id, t, n, out, h);
+    else if (wide) host_classify<2, true, true>(T, use_node, pred, cm, table_id, t, n, out, h);
     else if (uni) host_classify<2, true>(T, use_node, pred, cm, table_id, t, n, out, h);
     else host_classify<2, false>(T, use_node, pred, cm, table_id, t, n, out, h);
     return PG_OK;
@@ -760,7 +765,7 @@ int pg_node_common_stats(pg_ctx* ctx, uint64_t* base_image_bytes, uint64_t* comm
     uint64_t covered = 0, common = 0;
     for (size_t t = 0; t < h.tabs.size(); t++)
         if ((h.node.uniform ? h.node_aux : h.node_img)[h.node.tabinfo + 4 * t + 1] >> 31) covered++;
-    if (h.node.cmap && h.node.uniform)  // one 64-bit mask per IP class, in the class records
+    if (h.node.cmap && h.node.uniform)  // one 64-bit (wide records: 32-bit) mask per IP class, in the class records
         for (size_t g = 0; g < h.node.n_ipc; g++)
             for (size_t t = 0; t < h.tabs.size(); t++) {
                 const size_t b = t >> h.node.gshift;
@@ -806,7 +811,7 @@ int pg_node_uniform(pg_ctx* ctx) {
     Engine& E = ctx->eng;
     if (!E.compiled) E.compile();
     if (E.host.node_img.empty()) return fail(ctx, PG_ENOENT, "no node classifier (disabled or over budget)");
-    return E.host.node.uniform ? 1 : 0;
+    return E.host.node.uniform ? (E.host.node.wide ? 2 : 1) : 0;
     GUARD_END(ctx)
 }
 

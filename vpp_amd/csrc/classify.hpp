@@ -670,6 +670,14 @@ PG_HD End node_end_packed(uint32_t p) {
                tout == 0xFFu ? -1 : (int32_t)tout};
 }
 
+// wide class records (DevNode wide: 255 tables or more): interface index | kind << 14 (0xFFFF:
+// unresolved) in p, tin | tout << 16 in q (0xFFFF = no ACL)
+PG_HD End node_end_wide(uint32_t p, uint32_t q) {
+    const uint32_t f = p & 0xFFFFu, tin = q & 0xFFFFu, tout = q >> 16;
+    return End{f == 0xFFFFu ? -1 : (int32_t)((f & 0x3FFFu) | ((f >> 14) << kEndKindShift)),
+               tin == 0xFFFFu ? -1 : (int32_t)tin, tout == 0xFFFFu ? -1 : (int32_t)tout};
+}
+
 struct NoHook {
     PG_HD void operator()() const {}
 };
@@ -1105,8 +1113,10 @@ PG_HD void classify_q(const DevTableSet& T, const uint32_t* blobs, const DevTabl
 // only ones the node cannot classify) are left to the caller -- no evaluation, no count, a
 // placeholder verdict -- so the evaluation carries no per-table fallback (device.hip
 // PG_CONN_DEFER_ANY, PG_POD_DEFER_ANY)
+// WIDE (UNI): the node's wide class records (DevNode wide: 16-bit table ids in record word 3, the
+// common-row marks one 32-bit word)
 template <int MODE, bool COUNT, int Q, bool PRED = false, bool CM = false, bool NP = false, bool UNI = false,
-          bool DEFER = false, class L, class HS, class H = NoHook>
+          bool DEFER = false, bool WIDE = false, class L, class HS, class H = NoHook>
 PG_HD void classify_node_q(const DevTableSet& T, const DevNode& N, const L& img, const uint32_t (&s)[Q],
                            const uint32_t (&d)[Q], const uint32_t (&sp)[Q], const uint32_t (&dp)[Q],
                            const uint32_t (&pr)[Q], const HS& h, uint32_t (&out)[Q], const H& hook = H()) {
@@ -1180,7 +1190,18 @@ PG_HD void classify_node_q(const DevTableSet& T, const DevNode& N, const L& img,
     End es[Q], ed[Q];   // CONN: both end points; PERPOD: ed
     PG_UNROLL
     for (int j = 0; j < Q; j++) {
-        if constexpr (UNI) {  // record {self, packed end point, mask lo, mask hi}
+        if constexpr (UNI && WIDE) {  // record {self, interface, marks, tin | tout << 16}
+            if (MODE == 2) {
+                const W4 rs = img.u4_at_byte(rec[j]), rd = img.u4_at_byte(rec[Q + j]);
+                es[j] = node_end_wide(rs.y, rs.w), ed[j] = node_end_wide(rd.y, rd.w);
+                mks[j] = W2{rs.z, 0u}, mkd[j] = W2{rd.z, 0u};  // (T <= 32 << gshift: the low word only)
+            } else {
+                const W2 rd = img.u2_at_byte(rec[Q + j] + 8u);  // {marks, tables} of dst's record
+                ed[j] = node_end_wide(img.at_byte(rec[Q + j] + 4u), rd.y);
+                mks[j] = W2{CM ? img.at_byte(rec[j] + 8u) : 0u, 0u};
+                mkd[j] = mks[j];
+            }
+        } else if constexpr (UNI) {  // record {self, packed end point, mask lo, mask hi}
             if (MODE == 2) {
                 const W4 rs = img.u4_at_byte(rec[j]), rd = img.u4_at_byte(rec[Q + j]);
                 es[j] = node_end_packed(rs.y), ed[j] = node_end_packed(rd.y);

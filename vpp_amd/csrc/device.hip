@@ -624,12 +624,22 @@ constexpr int kernel_wpe_max() {
 #ifndef PG_CANDI_COMPACT
 #define PG_CANDI_COMPACT 1
 #endif
+// Active lanes: the grid-stride loop runs lane l of a wave while its group index q0 + l is below
+// nfull, so the lanes that reach this function always form a prefix 0 .. na-1 of the wave (the
+// last wave of a launch whose group count is not a multiple of 64 holds fewer). The walks are
+// spread over those na lanes only: lane i takes lookups r0 + i and r0 + na + i, r0 stepping by
+// 2 na, and the owner of lookup g pulls its verdict from lane (g - r0) mod na -- an inactive lane
+// would never walk the lookups given to it.
 template <bool COUNT, int P>
 __device__ __forceinline__ void classify_candi_group(const DevTableSet& T, const DevTable& tab0, uint8_t* scr,
                                                      const uint32_t (&s)[P], const uint32_t (&dp)[P],
                                                      const uint32_t (&pr)[P], const Hist& h, uint32_t (&out)[P]) {
+    // the scratch holds one byte per pending lookup (64 lanes x 4 slots = 256 B per wave, the
+    // launcher's BS * 4 bytes) and a byte encodes its owner as lane * 4 + slot
+    static_assert(P == 4, "classify_candi_group: 4 tuples per lane (scratch size, owner encoding)");
 #if defined(__HIP_DEVICE_COMPILE__)  // (device code only: wave intrinsics)
     const uint32_t lane = __lane_id();
+    const uint32_t na = (uint32_t)__popcll(__ballot(true));  // active lanes: 0 .. na-1
     const LdsLoader l0{};
     const DevLoader blob{T.blobs + tab0.blob_off};
     const uint32_t wb = tab0.kroot, wsz = tab0.nkc, woff = candi_window_off((tab0.fsk >> 8) & 0xFFu);
@@ -661,7 +671,7 @@ __device__ __forceinline__ void classify_candi_group(const DevTableSet& T, const
         M += (uint32_t)__popcll(m);
     }
     const BlobTab tb1{tab0.fsk, tab0.dflt, tab0.kroot, tab0.xoff, tab0.nkc, tab0.rule_base};
-    for (uint32_t r0 = 0; r0 < M; r0 += 128u) {
+    for (uint32_t r0 = 0; r0 < M; r0 += 2u * na) {
         uint32_t vs[2], vk[2], res[2] = {0u, 0u}, pos[2] = {0u, 0u};
         const uint32_t zero[2] = {0u, 0u};
         bool on[2], pd[2] = {false, false};
@@ -670,7 +680,7 @@ __device__ __forceinline__ void classify_candi_group(const DevTableSet& T, const
         const BlobTab tb[2] = {tb1, tb1};
 #pragma unroll
         for (int q = 0; q < 2; q++) {
-            const uint32_t gi = r0 + 64u * (uint32_t)q + lane;
+            const uint32_t gi = r0 + na * (uint32_t)q + lane;
             on[q] = gi < M;
             const uint32_t id = on[q] ? (uint32_t)scr[gi] : 0u;
             const int a = (int)((id >> 2) << 2);  // the owning lane, as a byte address
@@ -689,10 +699,11 @@ __device__ __forceinline__ void classify_candi_group(const DevTableSet& T, const
 #pragma unroll
         for (int j = 0; j < P; j++) {  // the owners pull their verdicts back
             const uint32_t rel = g[j] - r0;
-            const int a = (int)((rel & 63u) << 2);
+            const bool hi = rel >= na;
+            const int a = (int)(((hi ? rel - na : rel) & 63u) << 2);
             const uint32_t v0 = (uint32_t)__builtin_amdgcn_ds_bpermute(a, (int)res[0]);
             const uint32_t v1 = (uint32_t)__builtin_amdgcn_ds_bpermute(a, (int)res[1]);
-            if (pend[j] && rel < 128u) out[j] = rel < 64u ? v0 : v1;
+            if (pend[j] && rel < 2u * na) out[j] = hi ? v1 : v0;
         }
     }
 #pragma unroll
@@ -728,6 +739,8 @@ void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
     // PERPOD / CONN over a uniform node: ANY-protocol packets deferred to k_node_any
     // (PG_CONN_DEFER_ANY, PG_POD_DEFER_ANY)
     constexpr bool DEFER = UNIF && defer_any<MODE>();
+    // STAGE_ + 128 (uniform node): its wide class records (DevNode wide: 255 tables or more)
+    constexpr bool WIDE = UNIF && (STAGE_ & 128);
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     uint32_t* hist = smem + (STAGE ? stage_words : 0u);
     // node kernels: the LDS histogram, when used, holds every slot (HistT<true>: no window test)
@@ -902,9 +915,9 @@ void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
                 classify_candi_q<COUNT, QC>(T, LdsLoader{}, DevLoader{T.blobs + tab0.blob_off}, tab0, cs, cdp, cpr, h, co);
             } else if constexpr (NODE) {
                 if (c == (PG_HOOK_LAST ? P - QC : 0))
-                    classify_node_q<MODE, COUNT, QC, STAGE && PG_PRED, STAGE == 3, NOPAIR, UNIF, DEFER>(T, T.node, img, cs, cd, csp, cdp, cpr, h, co, hk);
+                    classify_node_q<MODE, COUNT, QC, STAGE && PG_PRED, STAGE == 3, NOPAIR, UNIF, DEFER, WIDE>(T, T.node, img, cs, cd, csp, cdp, cpr, h, co, hk);
                 else
-                    classify_node_q<MODE, COUNT, QC, STAGE && PG_PRED, STAGE == 3, NOPAIR, UNIF, DEFER>(T, T.node, img, cs, cd, csp, cdp, cpr, h, co);
+                    classify_node_q<MODE, COUNT, QC, STAGE && PG_PRED, STAGE == 3, NOPAIR, UNIF, DEFER, WIDE>(T, T.node, img, cs, cd, csp, cdp, cpr, h, co);
             } else {
                 classify_q<MODE, COUNT, QC, STAGE == 1 && PG_PRED>(T, blobs, tab0, cs, cd, csp, cdp, cpr, h, co, rootb);
             }
@@ -948,7 +961,7 @@ void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
         else if constexpr (FD) classify_fd_q<COUNT, 1>(T, LdsLoader{}, DevLoader{fd_blob}, tab0, s1, dp1, pr1, h, o);
         else if constexpr (MODE == 0 && STAGE == 6)
             classify_candi_q<COUNT, 1>(T, LdsLoader{}, DevLoader{T.blobs + tab0.blob_off}, tab0, s1, dp1, pr1, h, o);
-        else if constexpr (NODE) classify_node_q<MODE, COUNT, 1, STAGE && PG_PRED, STAGE == 3, NOPAIR, UNIF, DEFER>(T, T.node, img, s1, d1, sp1, dp1, pr1, h, o);
+        else if constexpr (NODE) classify_node_q<MODE, COUNT, 1, STAGE && PG_PRED, STAGE == 3, NOPAIR, UNIF, DEFER, WIDE>(T, T.node, img, s1, d1, sp1, dp1, pr1, h, o);
         else classify_q<MODE, COUNT, 1, STAGE == 1 && PG_PRED>(T, blobs, tab0, s1, d1, sp1, dp1, pr1, h, o, rootb);
         out[i] = o[0];
         if (DEFER && pr1[0] > 2u) *T.any_mark = T.any_seq;
@@ -1211,6 +1224,13 @@ static void launch_one(const DevTableSet& T, const Tuning& tu, int t, const uint
         // image copy then serves 16 waves (A/B on MI355X, the 10k-rule sweep table, 59.5 KB:
         // 393.8 -> 471.5 Gpps; config 2's 49 KB blob, three fit: 530 vs 475 at 1024)
         const size_t lds_bytes = hist + (size_t)stage * 4;
+        // (wide-record node builds, STAGE + 128: the per-mode workgroup size only -- block_stage is
+        // an A/B knob of the other builds, and every extra size is another set of kernels)
+        if constexpr (NODE && (STAGE & 128)) {
+            constexpr int BSW = node_wide<MODE, COUNT, NODE, STAGE>() ? PG_NODE_WIDE_BS : 512;
+            return launch_bs<MODE, COUNT, VEC, STAGE, NODE, BSW>(T, tu, t, src, dst, sport, dport, proto, n, out,
+                                                                 counters, st, hist, cells, stage, items);
+        }
         if constexpr (node_wide<MODE, COUNT, NODE, STAGE>() && PG_NODE_WIDE_BS != 1024)
             if (!tu.block_stage)
                 return launch_bs<MODE, COUNT, VEC, STAGE, NODE, PG_NODE_WIDE_BS>(T, tu, t, src, dst, sport, dport, proto,
@@ -1309,6 +1329,7 @@ static void launch_classify(const DevTableSet& T, const Tuning& tu, int t, const
         const bool nopair = T.node.n_pair == 0 && PG_NODE_NOPAIR;
         // (+ 64: the uniform cross layout, k_classify UNIF)
         const bool unif = T.node.uniform != 0;  // (no PAIR tables either; its tries take the aligned encoding)
+        const bool wide = unif && T.node.wide != 0;  // (+ 128: its wide class records, k_classify WIDE)
         auto go1 = [&](auto stage, const DevTableSet& Ts, uint32_t words) {
             constexpr int S = decltype(stage)::value;
             if constexpr (COUNT) {
@@ -1321,6 +1342,7 @@ static void launch_classify(const DevTableSet& T, const Tuning& tu, int t, const
         };
         auto go = [&](auto stage, const DevTableSet& Ts, uint32_t words) {
             constexpr int S = decltype(stage)::value;
+            if (wide) return go1(std::integral_constant<int, S + 96 + 128>{}, Ts, words);
             if (unif) return go1(std::integral_constant<int, S + 96>{}, Ts, words);
             if (nopair) return go1(std::integral_constant<int, S + 32>{}, Ts, words);
             go1(stage, Ts, words);

@@ -94,7 +94,7 @@ struct DevNode {
     // (record word p of the cross numbering is image word p - rec0 + lrec); launches that do not
     // stage that part of the image clear lrec and read the cross array
     uint32_t rec0, lrec;
-    // uniform layout (every table covered, none in PAIR form, fewer than 255 tables;
+    // uniform layout (every table covered, none in PAIR form, fewer than 65535 tables;
     // Tuning::node_uniform): table t's cross rows are over the node key classes, entry (t, ip
     // class g, key class k) at word (t * n_ipc + g) * gk + k, and its common row (when cmap != 0)
     // at image word crow0 + t * gk; tabinfo and kmap are not read, and the common-row marks are
@@ -103,6 +103,11 @@ struct DevNode {
     uint32_t uniform, crow0;
     uint32_t tstride;      // uniform layout: cross words per table, n_ipc * gk (below 2^24)
     uint32_t gshift;       // uniform layout: common-row mark bit of table t is t >> gshift (> 64 tables)
+    // uniform layout with 255 tables or more (wide records): a class record is {self, interface |
+    // kind << 14, marks (32 bits: bit t >> gshift, T <= 32 << gshift), tin | tout << 16 (0xFFFF =
+    // no ACL)} instead of {self, interface | kind << 14 | tin << 16 | tout << 24 (0xFF = no ACL),
+    // marks lo, marks hi} (classify.hpp node_end_packed / node_end_wide)
+    uint32_t wide;
     // list-verdict table (Tuning::node_list_table; 0 = the record form above): a kNodeList word's
     // low bits are a list id L, and its verdict for the rule's dst-side address is cross word
     // lv0 + L * n_ipc + (that address's node IP class) -- one gather, no record walk
@@ -219,10 +224,11 @@ struct Tuning {
     uint32_t pair = 1;             // PAIR for tables CROSS cannot take (0 = CAND, 2 = wherever it fits)
     uint32_t node_build = 1;       // build the node classifier (PERPOD / CONN)
     uint32_t node_root_bits = 12;  // its IPv4 / key trie root stride cap (4..16)
-    // uniform layout: cap of the key trie's root stride (2, 6 or 10). 10 saves a level (config 3
-    // +1 % in the driver's window) but its 4 KiB push config 5's image + counter histogram past
-    // the 80 KiB that keep two 1024-thread workgroups per CU (139 -> 94 Gpps)
-    uint32_t node_key_root_bits = 8;
+    // uniform layout: cap of the key trie's root stride, rounded down to 2, 6 or 10 (the strides
+    // build_node tries). 10 saves a level (config 3 +1 % in the driver's window) but its 4 KiB
+    // push config 5's image + counter histogram past the 80 KiB that keep two 1024-thread
+    // workgroups per CU (139 -> 94 Gpps)
+    uint32_t node_key_root_bits = 6;
     uint32_t node_common = 1;      // common-row section of node images
     uint32_t fd = 1;               // FD form of dst-independent CROSS tables that fit LDS
     uint32_t candi = 1;            // CANDI form (inline candidates) of dst-independent HBM-resident CAND tables

@@ -307,38 +307,51 @@ int Engine::sync() {
     const size_t slots = dev_view(cur).n_slots;
     // the counts of unchanged ACLs carry over to their new slots (slot_remap); changed and new
     // ones start at zero. The device counters keep their address while the slot count holds.
-    const bool carry = counters && counted_layout;  // (else: nothing counted yet, or a failed sync)
+    const bool carry = counters && counted_layout;  // (else: nothing counted yet)
     bool identity = false;
     std::vector<uint32_t> map;
     if (carry) map = slot_remap(*counted_layout, *layout, &identity);
-    counted_layout = nullptr;  // until the counters are in the new layout
+    // A failed step leaves the counters in the layout they were counted in (counted_layout and
+    // the buffer unchanged: the next sync carries them over again) -- except a remap in place
+    // that failed part-way, after which the counts restart
     if (!(carry && identity)) {
         unsigned long long* from = nullptr;  // the counts to carry: the old buffer or a copy of it
+        unsigned long long* into = counters;  // where the new layout's counts go
         if (carry && slots == counter_slots) {  // remap through a copy, into the same buffer
             from = (unsigned long long*)dev_alloc(counter_slots * 8, &err);
-            if (!from || dev_copy_d2d_async(from, counters, counter_slots * 8, nullptr, &err) != 0) {
+            if (!from || dev_copy_d2d_async(from, counters, counter_slots * 8, nullptr, &err) != 0 ||
+                dev_stream_sync(nullptr, &err) != 0) {
                 dev_release(from);
                 last_error = err;
                 return PG_ENOMEM;
             }
         } else if (slots != counter_slots || !counters) {
-            unsigned long long* nc = (unsigned long long*)dev_alloc(slots * sizeof(unsigned long long), &err);
-            if (!nc) {
+            into = (unsigned long long*)dev_alloc(slots * sizeof(unsigned long long), &err);
+            if (!into) {
                 last_error = err;
                 return PG_ENOMEM;
             }
             if (carry) from = counters;
-            else dev_release(counters);
-            counters = nc;
-            counter_slots = slots;
         }
-        int rc = from ? dev_counters_remap(counters, from, map.data(), slots, &err)
-                      : dev_memset(counters, 0, slots * 8, nullptr, &err);
+        int rc = from ? dev_counters_remap(into, from, map.data(), slots, &err)
+                      : dev_memset(into, 0, slots * 8, nullptr, &err);
         if (rc == 0) rc = dev_stream_sync(nullptr, &err);
-        dev_release(from);
         if (rc != 0) {
+            if (into != counters) {
+                dev_release(into);  // the old buffer, in its old layout, stays
+            } else {
+                dev_release(from);
+                counted_layout = nullptr;  // in place, part-way: the counts restart
+            }
             last_error = err;
             return PG_EIO;
+        }
+        if (into != counters) {  // the new buffer replaces the old one
+            dev_release(counters);
+            counters = into;
+            counter_slots = slots;
+        } else {
+            dev_release(from);
         }
     }
     counted_layout = layout;

@@ -932,8 +932,10 @@ void build_common_rows(HostTableSet& h, const std::vector<uint32_t>& cov, const 
     // 64 tables a bit covers a group of 2^gshift consecutive tables (bit t >> gshift): set when the
     // class's row is the common one in every table of the group, so an evaluation whose group bit
     // is clear gathers its entry from the cross table, which holds every row
+    // (wide records, DevNode wide: one 32-bit mark word, so T <= 32 << gshift)
+    const uint32_t mbits = N.wide ? 32u : 64u;
     uint32_t gshift = 0;
-    while (uni && (64u << gshift) < T) gshift++;
+    while (uni && (mbits << gshift) < T) gshift++;
     N.gshift = gshift;
     std::vector<uint32_t> masks(uni ? 2 * (size_t)G : 0, 0);
     std::vector<uint8_t> grp_common(uni ? (size_t)G * 64 : 0, 1);  // [g][group]: every table common
@@ -964,17 +966,20 @@ void build_common_rows(HostTableSet& h, const std::vector<uint32_t>& cov, const 
     }
     if (uni)
         for (uint32_t g = 0; g < G; g++)
-            for (uint32_t b = 0; b < 64 && (b << gshift) < T; b++)
+            for (uint32_t b = 0; b < mbits && (b << gshift) < T; b++)
                 if (grp_common[(size_t)g * 64 + b]) masks[2 * (size_t)g + (b >> 5)] |= 1u << (b & 31u);
     while (sec.size() % 4) sec.push_back(0);
     const uint32_t s0 = (uint32_t)img.size();
     for (uint32_t t : cov) TI[N.tabinfo + 4 * t + 2] = s0 + crow[t];
     img.insert(img.end(), sec.begin(), sec.end());
-    if (uni) {  // the masks live in the class records (words 2-3): class g's at word cmap + (g << 2)
+    if (uni) {  // the masks live in the class records (words 2-3; wide records: word 2, word 3 holds
+                // the end point's tables): class g's at word cmap + (g << 2)
         N.cmap = N.ipinfo + 2u;
         N.cmap_shift = 2u;
-        for (uint32_t g = 0; g < G; g++)
-            img[N.cmap + 4 * (size_t)g] = masks[2 * (size_t)g], img[N.cmap + 4 * (size_t)g + 1] = masks[2 * (size_t)g + 1];
+        for (uint32_t g = 0; g < G; g++) {
+            img[N.cmap + 4 * (size_t)g] = masks[2 * (size_t)g];
+            if (!N.wide) img[N.cmap + 4 * (size_t)g + 1] = masks[2 * (size_t)g + 1];
+        }
     } else {
         N.cmap = (uint32_t)img.size();
         N.cmap_shift = rs;
@@ -1131,11 +1136,13 @@ bool build_node(HostTableSet& h, const std::vector<TableAnalysis*>& an, const st
     // image: IPv4 trie (root at word 0), key trie, class records, tabinfo, kmap
     std::vector<uint32_t>& img = h.node_img;
     DevNode& N = h.node;
-    // end points pack into one record word (classify.hpp node_end_packed): interface indices
-    // below 2^14, fewer than 255 tables
-    bool pack_ok = T < 255;
+    // end points pack into the class record (classify.hpp node_end_packed): interface indices
+    // below 2^14; fewer than 255 tables in one word with the interface, else (wide records,
+    // DevNode wide) 16-bit table ids in a word of their own, beside 32-bit common-row marks
+    bool pack_ok = true;
     for (const auto& k : ipc_key)
         if ((int32_t)k[0] >= 0 && (k[0] & ~(3u << kEndKindShift)) >= 0x4000u) pack_ok = false;
+    const bool wide = T >= 255;  // (build_node: T < 0xFFFF, so 0xFFFF stays "no ACL")
     // uniform layout (DevNode uniform): every table covered, none in PAIR form -- rows over the
     // node key classes at cross[(t * G + ip class) * GK + key class], so an evaluation computes
     // its entry's address from (t, classes) instead of reading tabinfo and kmap (at most 64
@@ -1268,8 +1275,14 @@ bool build_node(HostTableSet& h, const std::vector<TableAnalysis*>& an, const st
         r[0] = node_entry(irec0 + rw * g, 0u, aligned);
         if (aligned) {
             auto t8 = [](uint32_t t) { return (int32_t)t < 0 ? 0xFFu : t; };
+            auto t16 = [](uint32_t t) { return (int32_t)t < 0 ? 0xFFFFu : t; };
             const uint32_t f = (int32_t)k[0] < 0 ? 0xFFFFu : ((k[0] & 0x3FFFu) | ((k[0] >> kEndKindShift) & 3u) << 14);
-            r[1] = f | t8(k[1]) << 16 | t8(k[2]) << 24;
+            if (wide) {
+                r[1] = f;
+                r[3] = t16(k[1]) | t16(k[2]) << 16;
+            } else {
+                r[1] = f | t8(k[1]) << 16 | t8(k[2]) << 24;
+            }
         }
     }
     for (uint32_t k = 0; k < GK; k++) img[krec0 + kw * k] = node_entry(krec0 + kw * k, 0u, aligned);
@@ -1307,6 +1320,7 @@ bool build_node(HostTableSet& h, const std::vector<TableAnalysis*>& an, const st
     N.gk = GK;
     N.n_ipc = G;
     N.n_pair = (uint32_t)PC;
+    N.wide = aligned && wide;
     N.img_words = N.img_words_base = (uint32_t)img.size();
     N.cmap = 0;
 

@@ -336,7 +336,8 @@ class Engine:
         lt = C.c_uint64()
         self._ck(lib.pg_node_list_table_stats(self.h, C.byref(lt)))
         st.update(list_table_bytes=lt.value)
-        st.update(uniform=bool(self._ck(lib.pg_node_uniform(self.h))))
+        u = self._ck(lib.pg_node_uniform(self.h))
+        st.update(uniform=bool(u), wide_records=u == 2)
         return st
 
     def slot_of_rule(self, tid, idx):

@@ -24,7 +24,7 @@ from . import renderer as R
 from ._capi import MODE_CONN, MODE_PERPOD, MODE_SINGLE
 
 SEEDS = {1: 0xC0DE0001, 2: 0xC0DE0002, 3: 0xC0DE0003, 4: 0xC0DE0004, 5: 0xC0DE0005, 6: 0xC0DE0006, 7: 0xC0DE0007,
-         8: 0xC0DE0008}
+         8: 0xC0DE0008, 9: 0xC0DE0009}
 POPULAR_PORTS = [22, 53, 67, 80, 81, 161, 162, 443, 514, 8080]
 
 
@@ -511,6 +511,18 @@ def config8(device=0, n_tuples=125 << 20, n_ns=10, apps=20):
                     local_ifs=local)
 
 
+def config9(device=0, n_tuples=125 << 20, n_ns=10, apps=50):
+    """Config 3's cluster with 50 apps per namespace: ~500 distinct per-pod tables (per-pod tables
+    are unbounded in the reference, cache_impl.go:409-466) -- past the 254 tables whose ids fit a
+    byte of the uniform layout's class record (its wide records: 16-bit table ids)."""
+    e, r, local, pool = cluster_engine(device, n_ns=n_ns, apps=apps)
+    gen = dict(seed=SEEDS[9], ip_pool=pool, pool_pct=85, dst_pool_pct=88,
+               port_pool=np.array(CLUSTER_PORTS, np.uint16), port_pool_pct=80, tcp_pct=60, udp_pct=30)
+    return Workload(9, e, MODE_PERPOD, -1, gen, n_tuples,
+                    "1k pods / 10 namespaces x 50 apps (~500 tables), evalACL on the dst interface", r,
+                    local_ifs=local)
+
+
 def config6(device=0, n_tuples=125 << 20, n_ns=10):
     """Config 3's shape given as K8s objects: namespace-wide selectors make
     the rule lists ~6.7x longer (64.6k rules in 52 tables)."""
@@ -534,4 +546,5 @@ def table_histogram(e):
     return dict(sorted(h.items()))
 
 
-CONFIGS = {1: config1, 2: config2, 3: config3, 4: config4, 5: config5, 6: config6, 7: config7, 8: config8}
+CONFIGS = {1: config1, 2: config2, 3: config3, 4: config4, 5: config5, 6: config6, 7: config7, 8: config8,
+           9: config9}
