@@ -639,7 +639,7 @@ DevTableSet host_view(const HostTableSet& h) {
 template <int MODE, int Q, bool PRED, bool CM, bool UNI, bool WIDE>
 void host_q(const DevTableSet& T, bool node, int table_id, const pg_tuple_soa* t, uint64_t i, uint32_t* out,
             const Hist& h) {
-    uint32_t s[Q], d[Q], sp[Q], dp[Q], pr[Q], o[Q];
+    uint32_t s[Q], d[Q], sp[Q], dp[Q], pr[Q], o[Q] = {};
     for (int j = 0; j < Q; j++) {
         s[j] = t->src_ip[i + j], d[j] = t->dst_ip[i + j], dp[j] = t->dst_port[i + j], pr[j] = t->proto[i + j];
         sp[j] = MODE == 2 ? t->src_port[i + j] : 0u;
@@ -653,9 +653,17 @@ void host_q(const DevTableSet& T, bool node, int table_id, const pg_tuple_soa* t
             classify_q<0, true, Q, PRED>(T, T.blobs, tab, s, d, sp, dp, pr, h, o);
         }
     } else {
-        if (node)
+        if (node && MODE == 2 && UNI) {
+            // as the device runs CONN over a uniform node: ANY-protocol packets deferred by the
+            // classify kernel to k_node_any (device.hip PG_CONN_DEFER_ANY), then classified
+            classify_node_q<MODE, true, Q, PRED, CM, false, UNI, true, WIDE>(T, T.node, DevLoader{T.node.img}, s, d, sp, dp,
+                                                                         pr, h, o);
+            for (int j = 0; j < Q; j++)
+                if (pr[j] > 2u) o[j] = conn_any_1<true>(T, s[j], d[j], h);
+        } else if (node) {
             classify_node_q<MODE, true, Q, PRED, CM, false, UNI, false, WIDE>(T, T.node, DevLoader{T.node.img}, s, d, sp, dp,
                                                                           pr, h, o);
+        }
         else classify_q<MODE, true, Q, PRED>(T, T.blobs, DevTable{}, s, d, sp, dp, pr, h, o);
     }
     for (int j = 0; j < Q; j++) out[i + j] = o[j];

@@ -999,6 +999,210 @@ PG_HD void conn_q(const DevTableSet& T, const EV& ev, const End (&es)[Q], const 
     }
 }
 
+#ifndef PG_CONN_UNI  // CONN over a uniform node: conn_uni_q (the packed end points as they are)
+#define PG_CONN_UNI 1
+#endif
+#ifndef PG_POD_UNI  // PERPOD over a uniform node: the same evaluation (uni_eval) on the dst record
+#define PG_POD_UNI 1
+#endif
+
+// One evalACL of tables t (NIL = no ACL: PERMIT, aclengine_mock.go:506-508) over the lanes `run`
+// of a uniform node (DevNode uniform): the cross-entry address from (table, IP class ca on the
+// rule's src side, key class g), read from the image when ca's common-row mark m for the table
+// is set, else from the cross array; a list resolves through the list-verdict table at the
+// rule-dst-side class cb. Counted (run lanes) into h. Key classes of valid keys only (the
+// callers leave ANY-protocol packets out of `run`).
+template <int Q, bool COUNT, bool CM, bool WIDE, class L, class HS>
+PG_HD void uni_eval(const DevTableSet& T, const DevNode& N, const L& img, const uint32_t (&t)[Q], const bool (&run)[Q],
+                    const uint32_t (&ca)[Q], const uint32_t (&cb)[Q], const uint32_t (&g)[Q], const W2 (&m)[Q],
+                    const HS& h, uint32_t (&w)[Q]) {
+    constexpr uint32_t NIL = WIDE ? 0xFFFFu : 0xFFu;
+    const DevLoader X{N.cross};
+    bool on[Q], cm[Q];
+    uint32_t pos[Q];
+    PG_UNROLL
+    for (int j = 0; j < Q; j++) {
+        on[j] = run[j] && t[j] != NIL;
+        uint32_t cw = 0;
+        if (CM) {  // bit t >> gshift of the class's marks (wide records: one 32-bit word)
+            const uint32_t tb = t[j] >> N.gshift;
+            cw = WIDE ? bit_of(m[j].x, tb) : bit_of(tb < 32u ? m[j].x : m[j].y, tb);
+        }
+        cm[j] = CM && cw != 0u;
+        // the common row's entry in the image, or the cross entry t * tstride + class * GK + k
+        const uint32_t pc = mad24(t[j], N.gk, N.crow0 + g[j]);
+        const uint32_t px = mad24(t[j], N.tstride, mad24(ca[j], N.gk, g[j]));
+        pos[j] = cm[j] ? pc : px;
+        if (run[j] && !on[j]) w[j] = verdict(kActPermit, T.slot_noacl);  // nil ACL
+    }
+    PG_UNROLL
+    for (int j = 0; j < Q; j++)
+        if (on[j] && !cm[j]) w[j] = X.u32(pos[j]);
+    if (CM) {
+        PG_UNROLL
+        for (int j = 0; j < Q; j++)
+            if (on[j] && cm[j]) w[j] = img.u32(pos[j]);
+    }
+    PG_UNROLL
+    for (int j = 0; j < Q; j++)  // a list: its verdict for the rule-dst-side address's class
+        if (on[j] && (w[j] & kNodeList)) w[j] = X.u32(N.lv0 + (w[j] & kNodeRecMask) * N.n_ipc + cb[j]);
+    if (COUNT) {
+        PG_UNROLL
+        for (int j = 0; j < Q; j++)
+            if (run[j]) h.inc_t(w[j] & kSlotMask, 0);
+    }
+}
+
+// The SYN-ACK half of a connection's testConnection over a uniform node, as a descriptor its
+// evaluations can run from anywhere -- another lane of the wave (device.hip PG_CONN_COMPACT) or
+// right away (conn_uni_q): the cross-entry position of each of the two evaluations (the dst
+// interface's inbound ACL, then the src interface's outbound ACL, both on the reversed packet:
+// the rule's src side is dst's class, the SYN-ACK key's class), flagged kDescCommon when it is
+// an image word (common row), kDescNil when the interface has no ACL; and e = the src class
+// (list verdicts) | run dst-inbound << 30 | run src-outbound << 31.
+constexpr uint32_t kDescNil = 0xFFFFFFFFu, kDescCommon = 1u << 31;
+struct ConnBack {
+    uint32_t d3, d4, e;
+    bool pend;  // a SYN-ACK evaluation remains (else out holds the final verdict)
+};
+template <bool CM, bool WIDE>
+PG_HD uint32_t uni_desc(const DevNode& N, uint32_t t, uint32_t ca, uint32_t g, const W2& m) {
+    constexpr uint32_t NIL = WIDE ? 0xFFFFu : 0xFFu;
+    if (t == NIL) return kDescNil;
+    uint32_t cw = 0;
+    if (CM) {
+        const uint32_t tb = t >> N.gshift;
+        cw = WIDE ? bit_of(m.x, tb) : bit_of(tb < 32u ? m.x : m.y, tb);
+    }
+    return cw ? (mad24(t, N.gk, N.crow0 + g) | kDescCommon) : mad24(t, N.tstride, mad24(ca, N.gk, g));
+}
+// the SYN-ACK evaluations of one pending connection (conn_q's last two steps): its ConnAction
+// word; counted into h
+template <bool COUNT, class L, class HS>
+PG_HD uint32_t conn_uni_back(const DevTableSet& T, const DevNode& N, const L& img, uint32_t d3, uint32_t d4, uint32_t e,
+                             const HS& h) {
+    const DevLoader X{N.cross};
+    const uint32_t cb = e & 0x3FFFFFFFu;
+    auto ev = [&](uint32_t dd) {
+        uint32_t v = verdict(kActPermit, T.slot_noacl);  // nil ACL (:506-508)
+        const bool nil = dd == kDescNil, com = !nil && (dd & kDescCommon);
+        if (!nil && !com) v = X.u32(dd);
+        if (com) v = img.u32(dd & ~kDescCommon);
+        if (!nil && (v & kNodeList)) v = X.u32(N.lv0 + (v & kNodeRecMask) * N.n_ipc + cb);
+        if (COUNT) h.inc_t(v & kSlotMask, 0);
+        return v;
+    };
+    uint32_t w = 0, res = 0;
+    bool go = true;
+    if ((e >> 30) & 1u) {  // SYN-ACK: dst interface inbound
+        w = ev(d3);
+        const uint32_t a = w >> 30;
+        if (a == kActFailure || a == kActDeny) {
+            res = verdict(a == kActFailure ? 3u : 1u, w & kSlotMask);
+            go = false;
+        }
+    }
+    if (go && (e >> 31)) {  // SYN-ACK: src interface outbound
+        w = ev(d4);
+        const uint32_t a = w >> 30;
+        res = verdict(a == kActFailure ? 3u : (a == kActDeny ? 1u : 2u), w & kSlotMask);
+    } else if (go) {
+        res = verdict(2u, w & kSlotMask);  // allowed; slot of the last evaluation
+    }
+    return res;
+}
+
+// testConnection (aclengine_mock.go:424-501) of Q connections over a uniform node's class
+// records, ANY-protocol packets deferred (device.hip PG_CONN_DEFER_ANY): conn_q's steps, run on
+// the records' packed end points as they are instead of decoded End structs -- the kinds of the
+// two interfaces add to 3 or more exactly when the pair has no Connection* call or an interface
+// is unresolved (0xFFFF has kind 3), "same interface" is equality of the 16-bit interface
+// fields, and a table id equal to NIL (0xFF; wide records 0xFFFF) is "no ACL". Every
+// evaluation computes its cross-entry address from (table, IP class, key class) and reads it
+// from the image when the class's common-row mark is set, else from the cross array; lists
+// resolve through the list-verdict table. The SYN half runs here; the SYN-ACK half is left in
+// `bk` (SPLIT: the caller runs conn_uni_back, device.hip PG_CONN_COMPACT) or run right away.
+// Same verdicts, slots and counts as conn_q over NodeEval (tests/test_node_host.py: node ==
+// per-table path == oracle).
+// rs / rd: the src / dst class records {self, packed end point, marks lo, marks hi} (wide:
+// {self, interface, marks, tin | tout << 16}); cs / cd: their classes; gs / ga: the key classes
+// of the SYN key (dport) and the SYN-ACK key (sport); dfr: deferred (no evaluation, no count).
+template <int Q, bool COUNT, bool CM, bool WIDE, bool SPLIT = false, class L, class HS>
+PG_HD void conn_uni_q(const DevTableSet& T, const DevNode& N, const L& img, const W4 (&rs)[Q], const W4 (&rd)[Q],
+                      const uint32_t (&cs)[Q], const uint32_t (&cd)[Q], const uint32_t (&gs)[Q],
+                      const uint32_t (&ga)[Q], const bool (&dfr)[Q], const HS& h, uint32_t (&out)[Q],
+                      ConnBack* bk = nullptr) {
+    bool live[Q], same[Q], srefl[Q], drefl[Q], run[Q];
+    uint32_t tsi[Q], tso[Q], tdi[Q], tdo[Q], t[Q], w[Q];
+    PG_UNROLL
+    for (int j = 0; j < Q; j++) {
+        const uint32_t ps = rs[j].y, pd = rd[j].y;
+        live[j] = !dfr[j] && ((ps >> 14) & 3u) + ((pd >> 14) & 3u) < 3u;
+        same[j] = ((ps ^ pd) & 0xFFFFu) == 0u;
+        if (WIDE) {
+            tsi[j] = rs[j].w & 0xFFFFu, tso[j] = rs[j].w >> 16, tdi[j] = rd[j].w & 0xFFFFu, tdo[j] = rd[j].w >> 16;
+        } else {
+            tsi[j] = (ps >> 16) & 0xFFu, tso[j] = ps >> 24, tdi[j] = (pd >> 16) & 0xFFu, tdo[j] = pd >> 24;
+        }
+        srefl[j] = drefl[j] = false;
+        w[j] = 0;
+        if (!live[j]) {
+            out[j] = verdict(3u, T.slot_unresolved);
+            if (COUNT && !dfr[j]) h.inc_cold(T.slot_unresolved);
+        }
+    }
+    W2 ms[Q], md[Q];  // the two classes' common-row marks
+    PG_UNROLL
+    for (int j = 0; j < Q; j++) ms[j] = W2{rs[j].z, rs[j].w}, md[j] = W2{rd[j].z, rd[j].w};
+    // SYN: src interface inbound (the rule's src side is the src class, the SYN key's class)
+    PG_UNROLL
+    for (int j = 0; j < Q; j++) t[j] = tsi[j], run[j] = live[j];
+    uni_eval<Q, COUNT, CM, WIDE>(T, N, img, t, run, cs, cd, gs, ms, h, w);
+    PG_UNROLL
+    for (int j = 0; j < Q; j++) {
+        if (!run[j]) continue;
+        const uint32_t a = w[j] >> 30;
+        if (a == kActFailure || a == kActDeny) {
+            out[j] = verdict(a == kActFailure ? 3u : 0u, w[j] & kSlotMask);
+            live[j] = false;
+        } else if (a == kActReflect) {
+            srefl[j] = true;
+            drefl[j] = same[j];
+        }
+    }
+    // SYN: dst interface outbound
+    PG_UNROLL
+    for (int j = 0; j < Q; j++) t[j] = tdo[j], run[j] = live[j] && !drefl[j];
+    uni_eval<Q, COUNT, CM, WIDE>(T, N, img, t, run, cs, cd, gs, ms, h, w);
+    PG_UNROLL
+    for (int j = 0; j < Q; j++) {
+        if (!run[j]) continue;
+        const uint32_t a = w[j] >> 30;
+        if (a == kActFailure || a == kActDeny) {
+            out[j] = verdict(a == kActFailure ? 3u : 0u, w[j] & kSlotMask);
+            live[j] = false;
+        } else if (a == kActReflect) {
+            drefl[j] = true;
+            if (same[j]) srefl[j] = true;
+        }
+    }
+    // the SYN-ACK half: allowed with the last evaluation's slot unless an evaluation remains
+    PG_UNROLL
+    for (int j = 0; j < Q; j++) {
+        ConnBack b;
+        b.pend = live[j] && (!drefl[j] || !srefl[j]);
+        if (live[j]) out[j] = verdict(2u, w[j] & kSlotMask);
+        b.d3 = uni_desc<CM, WIDE>(N, tdi[j], cd[j], ga[j], md[j]);
+        b.d4 = uni_desc<CM, WIDE>(N, tso[j], cd[j], ga[j], md[j]);
+        b.e = cs[j] | (uint32_t)!drefl[j] << 30 | (uint32_t)!srefl[j] << 31;
+        if constexpr (SPLIT) {
+            bk[j] = b;
+        } else {
+            if (b.pend) out[j] = conn_uni_back<COUNT>(T, N, img, b.d3, b.d4, b.e, h);
+        }
+    }
+}
+
 // evalACL of ANY-protocol packets (the L4 test skipped, aclengine_mock.go:562): the first rule
 // whose src and dst match, with its ANY action (engine.cpp compile_acl_rule) -- eval_linear's
 // ANY branch, inline: the CONN node build's deferred pass calls nothing (a call anywhere in a
@@ -1116,10 +1320,11 @@ PG_HD void classify_q(const DevTableSet& T, const uint32_t* blobs, const DevTabl
 // WIDE (UNI): the node's wide class records (DevNode wide: 16-bit table ids in record word 3, the
 // common-row marks one 32-bit word)
 template <int MODE, bool COUNT, int Q, bool PRED = false, bool CM = false, bool NP = false, bool UNI = false,
-          bool DEFER = false, bool WIDE = false, class L, class HS, class H = NoHook>
+          bool DEFER = false, bool WIDE = false, bool SPLIT = false, class L, class HS, class H = NoHook>
 PG_HD void classify_node_q(const DevTableSet& T, const DevNode& N, const L& img, const uint32_t (&s)[Q],
                            const uint32_t (&d)[Q], const uint32_t (&sp)[Q], const uint32_t (&dp)[Q],
-                           const uint32_t (&pr)[Q], const HS& h, uint32_t (&out)[Q], const H& hook = H()) {
+                           const uint32_t (&pr)[Q], const HS& h, uint32_t (&out)[Q], const H& hook = H(),
+                           ConnBack* bk = nullptr) {
     uint32_t key[Q], kack[Q];
     PG_UNROLL
     for (int j = 0; j < Q; j++) key[j] = pkt_key(pr[j], dp[j]), kack[j] = MODE == 2 ? pkt_key(pr[j], sp[j]) : key[j];
@@ -1186,6 +1391,52 @@ PG_HD void classify_node_q(const DevTableSet& T, const DevNode& N, const L& img,
     PG_UNROLL
     for (int j = 0; j < Q; j++) cs[j] = (rec[j] >> RS) - N.ipself, cd[j] = (rec[Q + j] >> RS) - N.ipself;
     bool hooked = false;
+    if constexpr (MODE == 2 && UNI && DEFER && PG_CONN_UNI) {  // CONN over the class records as they are
+        W4 rs[Q], rd[Q];
+        bool dfr[Q];
+        PG_UNROLL
+        for (int j = 0; j < Q; j++) {
+            rs[j] = img.u4_at_byte(rec[j]), rd[j] = img.u4_at_byte(rec[Q + j]);
+            dfr[j] = key[j] >= kWalkKeyLimit || kack[j] >= kWalkKeyLimit;
+        }
+        conn_uni_q<Q, COUNT, CM, WIDE, SPLIT>(T, N, img, rs, rd, cs, cd, gs, ga, dfr, h, out, bk);
+        hook();
+        return;
+    }
+    if constexpr (MODE == 1 && UNI && PG_POD_UNI) {  // PERPOD: the dst record's outbound table as it is
+        constexpr uint32_t NIL = WIDE ? 0xFFFFu : 0xFFu;
+        uint32_t t[Q];
+        bool run[Q], fbk[Q];
+        W2 ms[Q];
+        PG_UNROLL
+        for (int j = 0; j < Q; j++) {
+            const uint32_t pd = img.at_byte(rec[Q + j] + 4u);  // interface | kind << 14 (0xFFFF: unresolved)
+            t[j] = WIDE ? img.at_byte(rec[Q + j] + 12u) >> 16 : pd >> 24;
+            ms[j] = !CM ? W2{0u, 0u} : (WIDE ? W2{img.at_byte(rec[j] + 8u), 0u} : img.u2_at_byte(rec[j] + 8u));
+            const bool df = DEFER && key[j] >= kWalkKeyLimit;  // (deferred: left to the caller)
+            run[j] = !df && (pd & 0xFFFFu) != 0xFFFFu;
+            if (!run[j]) {
+                out[j] = verdict(kActFailure, T.slot_unresolved);
+                if (COUNT && !df) h.inc_cold(T.slot_unresolved);
+            }
+            // ANY-protocol packets (no key class) on a table: the per-table path below
+            fbk[j] = run[j] && key[j] >= kWalkKeyLimit && t[j] != NIL;
+            run[j] = run[j] && !fbk[j];
+        }
+        uni_eval<Q, COUNT, CM, WIDE>(T, N, img, t, run, cs, cd, gs, ms, h, out);
+        bool anyfb = false;
+        PG_UNROLL
+        for (int j = 0; j < Q; j++) anyfb |= fbk[j];
+        if (!DEFER && anyfb) {
+            for (int j = 0; j < Q; j++) {
+                if (!fbk[j]) continue;
+                out[j] = eval_one(T.rules, T.blobs, T.tabs, (int32_t)t[j], s[j], d[j], key[j]);
+                if (COUNT) h.inc_t(out[j] & kSlotMask, (int32_t)t[j]);
+            }
+        }
+        hook();
+        return;
+    }
     W2 mks[Q], mkd[Q];  // UNI: the common-row masks of the two classes, read once per tuple
     End es[Q], ed[Q];   // CONN: both end points; PERPOD: ed
     PG_UNROLL
