@@ -1053,65 +1053,6 @@ PG_HD void uni_eval(const DevTableSet& T, const DevNode& N, const L& img, const 
     }
 }
 
-// The SYN-ACK half of a connection's testConnection over a uniform node, as a descriptor its
-// evaluations can run from anywhere -- another lane of the wave (device.hip PG_CONN_COMPACT) or
-// right away (conn_uni_q): the cross-entry position of each of the two evaluations (the dst
-// interface's inbound ACL, then the src interface's outbound ACL, both on the reversed packet:
-// the rule's src side is dst's class, the SYN-ACK key's class), flagged kDescCommon when it is
-// an image word (common row), kDescNil when the interface has no ACL; and e = the src class
-// (list verdicts) | run dst-inbound << 30 | run src-outbound << 31.
-constexpr uint32_t kDescNil = 0xFFFFFFFFu, kDescCommon = 1u << 31;
-struct ConnBack {
-    uint32_t d3, d4, e;
-    bool pend;  // a SYN-ACK evaluation remains (else out holds the final verdict)
-};
-template <bool CM, bool WIDE>
-PG_HD uint32_t uni_desc(const DevNode& N, uint32_t t, uint32_t ca, uint32_t g, const W2& m) {
-    constexpr uint32_t NIL = WIDE ? 0xFFFFu : 0xFFu;
-    if (t == NIL) return kDescNil;
-    uint32_t cw = 0;
-    if (CM) {
-        const uint32_t tb = t >> N.gshift;
-        cw = WIDE ? bit_of(m.x, tb) : bit_of(tb < 32u ? m.x : m.y, tb);
-    }
-    return cw ? (mad24(t, N.gk, N.crow0 + g) | kDescCommon) : mad24(t, N.tstride, mad24(ca, N.gk, g));
-}
-// the SYN-ACK evaluations of one pending connection (conn_q's last two steps): its ConnAction
-// word; counted into h
-template <bool COUNT, class L, class HS>
-PG_HD uint32_t conn_uni_back(const DevTableSet& T, const DevNode& N, const L& img, uint32_t d3, uint32_t d4, uint32_t e,
-                             const HS& h) {
-    const DevLoader X{N.cross};
-    const uint32_t cb = e & 0x3FFFFFFFu;
-    auto ev = [&](uint32_t dd) {
-        uint32_t v = verdict(kActPermit, T.slot_noacl);  // nil ACL (:506-508)
-        const bool nil = dd == kDescNil, com = !nil && (dd & kDescCommon);
-        if (!nil && !com) v = X.u32(dd);
-        if (com) v = img.u32(dd & ~kDescCommon);
-        if (!nil && (v & kNodeList)) v = X.u32(N.lv0 + (v & kNodeRecMask) * N.n_ipc + cb);
-        if (COUNT) h.inc_t(v & kSlotMask, 0);
-        return v;
-    };
-    uint32_t w = 0, res = 0;
-    bool go = true;
-    if ((e >> 30) & 1u) {  // SYN-ACK: dst interface inbound
-        w = ev(d3);
-        const uint32_t a = w >> 30;
-        if (a == kActFailure || a == kActDeny) {
-            res = verdict(a == kActFailure ? 3u : 1u, w & kSlotMask);
-            go = false;
-        }
-    }
-    if (go && (e >> 31)) {  // SYN-ACK: src interface outbound
-        w = ev(d4);
-        const uint32_t a = w >> 30;
-        res = verdict(a == kActFailure ? 3u : (a == kActDeny ? 1u : 2u), w & kSlotMask);
-    } else if (go) {
-        res = verdict(2u, w & kSlotMask);  // allowed; slot of the last evaluation
-    }
-    return res;
-}
-
 // testConnection (aclengine_mock.go:424-501) of Q connections over a uniform node's class
 // records, ANY-protocol packets deferred (device.hip PG_CONN_DEFER_ANY): conn_q's steps, run on
 // the records' packed end points as they are instead of decoded End structs -- the kinds of the
@@ -1120,18 +1061,17 @@ PG_HD uint32_t conn_uni_back(const DevTableSet& T, const DevNode& N, const L& im
 // fields, and a table id equal to NIL (0xFF; wide records 0xFFFF) is "no ACL". Every
 // evaluation computes its cross-entry address from (table, IP class, key class) and reads it
 // from the image when the class's common-row mark is set, else from the cross array; lists
-// resolve through the list-verdict table. The SYN half runs here; the SYN-ACK half is left in
-// `bk` (SPLIT: the caller runs conn_uni_back, device.hip PG_CONN_COMPACT) or run right away.
-// Same verdicts, slots and counts as conn_q over NodeEval (tests/test_node_host.py: node ==
+// resolve through the list-verdict table. (Two schedules that ran the SYN-ACK half elsewhere --
+// numbered wave-wide and run on other lanes, or the last evaluation in a per-lane loop after all
+// of a lane's connections -- measured slower on MI355X, DESIGN.md Appendix A.) Same verdicts, slots and counts as conn_q over NodeEval (tests/test_node_host.py: node ==
 // per-table path == oracle).
 // rs / rd: the src / dst class records {self, packed end point, marks lo, marks hi} (wide:
 // {self, interface, marks, tin | tout << 16}); cs / cd: their classes; gs / ga: the key classes
 // of the SYN key (dport) and the SYN-ACK key (sport); dfr: deferred (no evaluation, no count).
-template <int Q, bool COUNT, bool CM, bool WIDE, bool SPLIT = false, class L, class HS>
+template <int Q, bool COUNT, bool CM, bool WIDE, class L, class HS>
 PG_HD void conn_uni_q(const DevTableSet& T, const DevNode& N, const L& img, const W4 (&rs)[Q], const W4 (&rd)[Q],
                       const uint32_t (&cs)[Q], const uint32_t (&cd)[Q], const uint32_t (&gs)[Q],
-                      const uint32_t (&ga)[Q], const bool (&dfr)[Q], const HS& h, uint32_t (&out)[Q],
-                      ConnBack* bk = nullptr) {
+                      const uint32_t (&ga)[Q], const bool (&dfr)[Q], const HS& h, uint32_t (&out)[Q]) {
     bool live[Q], same[Q], srefl[Q], drefl[Q], run[Q];
     uint32_t tsi[Q], tso[Q], tdi[Q], tdo[Q], t[Q], w[Q];
     PG_UNROLL
@@ -1186,20 +1126,30 @@ PG_HD void conn_uni_q(const DevTableSet& T, const DevNode& N, const L& img, cons
             if (same[j]) srefl[j] = true;
         }
     }
-    // the SYN-ACK half: allowed with the last evaluation's slot unless an evaluation remains
+    // SYN-ACK: dst interface inbound (reversed packet: the rule's src side is the dst class, the
+    // SYN-ACK key's class)
+    PG_UNROLL
+    for (int j = 0; j < Q; j++) t[j] = tdi[j], run[j] = live[j] && !drefl[j];
+    uni_eval<Q, COUNT, CM, WIDE>(T, N, img, t, run, cd, cs, ga, md, h, w);
     PG_UNROLL
     for (int j = 0; j < Q; j++) {
-        ConnBack b;
-        b.pend = live[j] && (!drefl[j] || !srefl[j]);
-        if (live[j]) out[j] = verdict(2u, w[j] & kSlotMask);
-        b.d3 = uni_desc<CM, WIDE>(N, tdi[j], cd[j], ga[j], md[j]);
-        b.d4 = uni_desc<CM, WIDE>(N, tso[j], cd[j], ga[j], md[j]);
-        b.e = cs[j] | (uint32_t)!drefl[j] << 30 | (uint32_t)!srefl[j] << 31;
-        if constexpr (SPLIT) {
-            bk[j] = b;
-        } else {
-            if (b.pend) out[j] = conn_uni_back<COUNT>(T, N, img, b.d3, b.d4, b.e, h);
+        if (!run[j]) continue;
+        const uint32_t a = w[j] >> 30;
+        if (a == kActFailure || a == kActDeny) {
+            out[j] = verdict(a == kActFailure ? 3u : 1u, w[j] & kSlotMask);
+            live[j] = false;
         }
+    }
+    // SYN-ACK: src interface outbound
+    PG_UNROLL
+    for (int j = 0; j < Q; j++) t[j] = tso[j], run[j] = live[j] && !srefl[j];
+    uni_eval<Q, COUNT, CM, WIDE>(T, N, img, t, run, cd, cs, ga, md, h, w);
+    PG_UNROLL
+    for (int j = 0; j < Q; j++) {
+        if (!live[j]) continue;
+        const uint32_t a = w[j] >> 30;
+        if (run[j] && (a == kActFailure || a == kActDeny)) out[j] = verdict(a == kActFailure ? 3u : 1u, w[j] & kSlotMask);
+        else out[j] = verdict(2u, w[j] & kSlotMask);  // allowed; slot of the last evaluation
     }
 }
 
@@ -1320,11 +1270,10 @@ PG_HD void classify_q(const DevTableSet& T, const uint32_t* blobs, const DevTabl
 // WIDE (UNI): the node's wide class records (DevNode wide: 16-bit table ids in record word 3, the
 // common-row marks one 32-bit word)
 template <int MODE, bool COUNT, int Q, bool PRED = false, bool CM = false, bool NP = false, bool UNI = false,
-          bool DEFER = false, bool WIDE = false, bool SPLIT = false, class L, class HS, class H = NoHook>
+          bool DEFER = false, bool WIDE = false, class L, class HS, class H = NoHook>
 PG_HD void classify_node_q(const DevTableSet& T, const DevNode& N, const L& img, const uint32_t (&s)[Q],
                            const uint32_t (&d)[Q], const uint32_t (&sp)[Q], const uint32_t (&dp)[Q],
-                           const uint32_t (&pr)[Q], const HS& h, uint32_t (&out)[Q], const H& hook = H(),
-                           ConnBack* bk = nullptr) {
+                           const uint32_t (&pr)[Q], const HS& h, uint32_t (&out)[Q], const H& hook = H()) {
     uint32_t key[Q], kack[Q];
     PG_UNROLL
     for (int j = 0; j < Q; j++) key[j] = pkt_key(pr[j], dp[j]), kack[j] = MODE == 2 ? pkt_key(pr[j], sp[j]) : key[j];
@@ -1399,7 +1348,7 @@ PG_HD void classify_node_q(const DevTableSet& T, const DevNode& N, const L& img,
             rs[j] = img.u4_at_byte(rec[j]), rd[j] = img.u4_at_byte(rec[Q + j]);
             dfr[j] = key[j] >= kWalkKeyLimit || kack[j] >= kWalkKeyLimit;
         }
-        conn_uni_q<Q, COUNT, CM, WIDE, SPLIT>(T, N, img, rs, rd, cs, cd, gs, ga, dfr, h, out, bk);
+        conn_uni_q<Q, COUNT, CM, WIDE>(T, N, img, rs, rd, cs, cd, gs, ga, dfr, h, out);
         hook();
         return;
     }

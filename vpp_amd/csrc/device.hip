@@ -717,79 +717,6 @@ __device__ __forceinline__ void classify_candi_group(const DevTableSet& T, const
 #endif
 }
 
-// CONN over a uniform node (every table covered, ANY-protocol packets deferred): the SYN-ACK
-// half of testConnection compacted across the wave (PG_CONN_COMPACT). The SYN half (classify.hpp
-// conn_uni_q: both end points' records, the src inbound and dst outbound evaluations) runs for
-// each of the lane's P connections in turn and leaves a descriptor of the rest (ConnBack); 22 %
-// of config 5's connections go on to the dst interface's inbound ACL and 2.3 % to the src
-// interface's outbound ACL, but with 64 lanes nearly every wave ran both evaluation blocks for
-// each of its P slots, every lane paying their instructions. Here the pending connections are
-// numbered wave-wide (a ballot and mbcnt per slot), lane i runs conn_uni_back for the i-th
-// (descriptor pulled from its owner with ds_bpermute, the owner found through a byte of the
-// wave's 64-B LDS scratch), counts its evaluations, and the owners pull the ConnAction words
-// back: one pass over the wave for up to 64 pending connections instead of P. The active lanes
-// form a prefix 0 .. na-1 of the wave (classify_candi_group), and the walks go to them only.
-#ifndef PG_CONN_COMPACT
-#define PG_CONN_COMPACT 1
-#endif
-template <int MODE, int STAGE>
-constexpr bool conn_compact() {
-    return MODE == 2 && (STAGE & 32) && (STAGE & 64) && defer_any<2>() && PG_CONN_UNI && PG_CONN_COMPACT;
-}
-template <bool COUNT, bool CM, bool WIDE, int P, class L, class HS>
-__device__ __forceinline__ void conn_uni_group(const DevTableSet& T, const L& img, uint8_t* scr, const uint32_t (&s)[P],
-                                               const uint32_t (&d)[P], const uint32_t (&sp)[P], const uint32_t (&dp)[P],
-                                               const uint32_t (&pr)[P], const HS& h, uint32_t (&out)[P]) {
-    static_assert(P <= 4, "conn_uni_group: an owner byte is lane * 4 + slot");
-#if defined(__HIP_DEVICE_COMPILE__)  // (device code only: wave intrinsics)
-    const DevNode& N = T.node;
-    ConnBack bk[P];
-#pragma unroll
-    for (int j = 0; j < P; j++) {  // the SYN half, one connection at a time (registers)
-        const uint32_t s1[1] = {s[j]}, d1[1] = {d[j]}, sp1[1] = {sp[j]}, dp1[1] = {dp[j]}, pr1[1] = {pr[j]};
-        uint32_t o1[1];
-        classify_node_q<2, COUNT, 1, false, CM, true, true, true, WIDE, true>(T, N, img, s1, d1, sp1, dp1, pr1, h, o1,
-                                                                             NoHook(), &bk[j]);
-        out[j] = o1[0];
-    }
-    const uint32_t lane = __lane_id();
-    const uint32_t na = (uint32_t)__popcll(__ballot(true));  // active lanes: 0 .. na-1
-    uint32_t g[P], M = 0;  // the pending connections' numbers; M of them in the wave (uniform)
-#pragma unroll
-    for (int j = 0; j < P; j++) {
-        const unsigned long long m = __ballot(bk[j].pend);
-        g[j] = M + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-        M += (uint32_t)__popcll(m);
-    }
-    for (uint32_t r0 = 0; r0 < M; r0 += na) {
-#pragma unroll
-        for (int j = 0; j < P; j++) {
-            const uint32_t rel = g[j] - r0;
-            if (bk[j].pend && rel < na) scr[rel] = (uint8_t)(lane * 4u + (uint32_t)j);
-        }
-        const bool on = r0 + lane < M;
-        const uint32_t id = on ? (uint32_t)scr[lane] : 0u;
-        const int a = (int)((id >> 2) << 2);  // the owner lane, as a byte address
-        uint32_t x3 = 0, x4 = 0, xe = 0;
-#pragma unroll
-        for (int j = 0; j < P; j++) {
-            const uint32_t p3 = (uint32_t)__builtin_amdgcn_ds_bpermute(a, (int)bk[j].d3);
-            const uint32_t p4 = (uint32_t)__builtin_amdgcn_ds_bpermute(a, (int)bk[j].d4);
-            const uint32_t pe = (uint32_t)__builtin_amdgcn_ds_bpermute(a, (int)bk[j].e);
-            if ((id & 3u) == (uint32_t)j) x3 = p3, x4 = p4, xe = pe;
-        }
-        uint32_t res = 0;
-        if (on) res = conn_uni_back<COUNT>(T, N, img, x3, x4, xe, h);
-#pragma unroll
-        for (int j = 0; j < P; j++) {  // the owners pull their ConnAction words back
-            const uint32_t rel = g[j] - r0;
-            const uint32_t v = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((rel & 63u) << 2), (int)res);
-            if (bk[j].pend && rel < na) out[j] = v;
-        }
-    }
-#endif
-}
-
 template <int MODE, bool COUNT, bool VEC, int STAGE_, bool NODE, int BS>
 __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(kernel_wpe<MODE, COUNT, NODE, STAGE_>(),
                                                                     kernel_wpe_max<MODE, COUNT, NODE, STAGE_>())))
@@ -855,10 +782,9 @@ void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
     const bool cache = NODE && COUNT && !lds_hist && hist_cells != 0;
     const bool has_hist = COUNT && (!NODE || lds_hist || cache);  // an LDS histogram was allocated
     // STAGE 6 (PG_CANDI_COMPACT): each wave's 256-B scratch after the staged words and histogram
-    // (cells + 2 words; a slot cache: 2 (cells + 1)); CONN over a uniform node (PG_CONN_COMPACT): 64 B
-    constexpr uint32_t kScr = NODE ? 64u : 256u;
+    // (cells + 2 words; a node slot cache would take 2 (cells + 1))
     const uint32_t hist_words = !has_hist ? 0u : (cache ? 2u * (hist_cells + 1u) : hist_cells + 2u);
-    uint8_t* const cscr = reinterpret_cast<uint8_t*>(smem + stage_words + hist_words) + (threadIdx.x >> 6) * kScr;
+    uint8_t* const cscr = reinterpret_cast<uint8_t*>(smem + stage_words + hist_words) + (threadIdx.x >> 6) * 256u;
     const uint32_t wn = COUNT ? hist_cells : 0u;
     const uint32_t wbase = (MODE == 0 && wn < T.n_slots) ? min(tab0.rule_base, T.n_slots - wn) : 0u;
     const uint32_t xslot = MODE == 0 ? (tab0.dflt & kSlotMask) : T.slot_noacl;
@@ -976,8 +902,6 @@ void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
                                                                         : PG_QSINGLE)));
         if constexpr (MODE == 0 && STAGE == 6 && PG_CANDI_COMPACT) {
             classify_candi_group<COUNT, P>(T, tab0, cscr, sv, dpv, prv, h, o);
-        } else if constexpr (NODE && conn_compact<MODE, STAGE_>()) {
-            conn_uni_group<COUNT, STAGE == 3, WIDE, P>(T, img, cscr, sv, dv, spv, dpv, prv, h, o);
         } else
 #pragma unroll
         for (int c = 0; c < P; c += QC) {
@@ -1271,9 +1195,8 @@ static void launch_bs(const DevTableSet& T, const Tuning& tu, int t, const uint3
     // the three LDS would allow (A/B on MI355X, config 2: 541-546 vs 533-535 Gpps, repeated
     // three times; with counters no difference): fewer streams in flight per CU contend less
     const uint32_t bpc = tu.blocks_per_cu ? tu.blocks_per_cu : (MODE == 0 && (STAGE & 7) == 4 && !COUNT ? 2u : 0u);
-    // (STAGE 6 with PG_CANDI_COMPACT: + 256 B of scratch per wave; CONN with PG_CONN_COMPACT: + 64 B)
-    const size_t lds = hist + (size_t)stage * 4 + (!NODE && (STAGE & 7) == 6 && PG_CANDI_COMPACT ? (size_t)BS * 4 : 0) +
-                       (NODE && conn_compact<MODE, STAGE>() ? (size_t)BS : 0);
+    // (STAGE 6 with PG_CANDI_COMPACT: + 256 B of scratch per wave)
+    const size_t lds = hist + (size_t)stage * 4 + (!NODE && (STAGE & 7) == 6 && PG_CANDI_COMPACT ? (size_t)BS * 4 : 0);
     // PERPOD / CONN over a uniform node: k_node_any after the classify kernel, for its deferred
     // ANY-protocol packets (PG_CONN_DEFER_ANY, PG_POD_DEFER_ANY; the launch's mark word and
     // number: dev_classify)
