@@ -842,13 +842,15 @@ bool build_fd_blob(const TableAnalysis& A, uint32_t dflt, const Tuning& tu, std:
                    uint32_t max_words, uint32_t lds_words) {
     if (A.pair || !A.clist.empty() || A.nsc == 0 || A.nkc == 0) return false;  // dst lists: the verdict reads dst
     // trie shapes, fewest levels first: the first whose blob fits LDS (lds_words) is taken;
-    // if none does, the first that fits max_words (read from HBM, its prefix staged)
+    // if none does, of those that fit max_words (read from HBM, its prefix staged) the one with
+    // the fewest dependent reads, then the smallest
     struct Shape {
         bool lc;
         uint32_t s1max, cstride;
     };
     const Shape shapes[] = {{true, 12, 8}, {false, 12, 8}, {false, 10, 6}, {false, 8, 4}};
     std::vector<uint32_t> best;
+    uint64_t best_key = ~0ull;
     for (const Shape& sh : shapes) {
         const bool lc = sh.lc;
         const uint32_t s1 = std::min<uint32_t>(pick_stride(A.sb.size(), 32, tu), sh.s1max);
@@ -892,8 +894,21 @@ bool build_fd_blob(const TableAnalysis& A, uint32_t dflt, const Tuning& tu, std:
         blob[8] = A.nkc;
         blob[9] = (P + K + 3u) & ~3u;
         blob[10] = A.nsc;
+        if (std::getenv("PG_FD_DEBUG")) {  // measurement aid: where an FD blob's words go
+            std::set<std::vector<uint32_t>> rows;
+            for (uint32_t c = 0; c < A.nsc; c++)
+                rows.insert(std::vector<uint32_t>(A.cverd.begin() + (size_t)c * A.nkc,
+                                                  A.cverd.begin() + (size_t)(c + 1) * A.nkc));
+            std::fprintf(stderr, "fd: lc %d s1 %u k1 %u depths %u/%u | words: prefix %u, src levels %u, rows %u, total %zu "
+                                 "(%u classes, %zu distinct rows, %u key classes)\n",
+                         (int)lc, s1, k1, ds, dk, P + K, below, A.nsc * rstep, blob.size(), A.nsc, rows.size(), A.nkc);
+        }
         if (blob.size() <= lds_words) return true;
-        if (best.empty()) best.swap(blob);
+        // read from HBM / L2: the fewest dependent reads, then the smallest blob -- a wider
+        // (level-compressed) shape of the same depth only spreads the gathers over more bytes
+        // than an XCD's L2 holds (config 7: 6.3 MB level-compressed vs 4.2 MB, both 4 / 3 reads)
+        const uint64_t key = (uint64_t)std::max(ds, dk) << 40 | (uint64_t)(ds + dk) << 32 | blob.size();
+        if (best.empty() || key < best_key) best.swap(blob), best_key = key;
     }
     if (best.empty()) return false;
     blob.swap(best);
