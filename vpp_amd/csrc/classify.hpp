@@ -374,6 +374,22 @@ struct HistT {
 #endif
         inc(slot);
     }
+    // one increment of the slot of verdict word w (bits 29-0). The CONN full-histogram build
+    // compares w << 2 -- the slot's byte offset, the action bits shifted out -- with the two
+    // register-counted slots' offsets and adds at that offset: no mask of the action bits
+    PG_HD void inc_w(uint32_t w) const {
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(PG_PROBE_NOINC)
+        if constexpr (kFullOnly && kHotRegs) {
+            const uint32_t b = w << 2;
+            nhot += b == hot << 2;
+            nhot2 += b == hot2 << 2;
+            if (b != hot << 2 && b != hot2 << 2)
+                atomicAdd(reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(lds) + b), 1u);
+            return;
+        }
+#endif
+        inc_t(w & 0x3FFFFFFFu, 0);
+    }
     PG_HD void inc(uint32_t slot) const {
 #if defined(__HIP_DEVICE_COMPILE__) && defined(PG_PROBE_NOINC)  // measurement build only
         if (slot == 0xFFFFFFFFu) lds[0] = 0;
@@ -1049,9 +1065,12 @@ PG_HD void uni_eval(const DevTableSet& T, const DevNode& N, const L& img, const 
     if (COUNT) {
         PG_UNROLL
         for (int j = 0; j < Q; j++)
-            if (run[j]) h.inc_t(w[j] & kSlotMask, 0);
+            if (run[j]) h.inc_w(w[j]);
     }
 }
+// an evaluation's ACLAction stops testConnection: DENY (0) or FAILURE (3) -- w + 2^30 then has
+// bit 31 clear (PERMIT and REFLECT set it)
+PG_HD bool conn_stop(uint32_t w) { return (w + 0x40000000u) < 0x80000000u; }
 
 // testConnection (aclengine_mock.go:424-501) of Q connections over a uniform node's class
 // records, ANY-protocol packets deferred (device.hip PG_CONN_DEFER_ANY): conn_q's steps, run on
@@ -1094,21 +1113,20 @@ PG_HD void conn_uni_q(const DevTableSet& T, const DevNode& N, const L& img, cons
     W2 ms[Q], md[Q];  // the two classes' common-row marks
     PG_UNROLL
     for (int j = 0; j < Q; j++) ms[j] = W2{rs[j].z, rs[j].w}, md[j] = W2{rd[j].z, rd[j].w};
-    // SYN: src interface inbound (the rule's src side is the src class, the SYN key's class)
+    // SYN: src interface inbound (the rule's src side is the src class, the SYN key's class). A
+    // SYN evaluation that stops the connection gives its ConnAction in the ACLAction bits as they
+    // are (DENY 0 -> DenySyn 0, FAILURE 3 -> Failure 3); a SYN-ACK one ORs in 1 (-> DenySynAck 1,
+    // Failure 3)
     PG_UNROLL
     for (int j = 0; j < Q; j++) t[j] = tsi[j], run[j] = live[j];
     uni_eval<Q, COUNT, CM, WIDE>(T, N, img, t, run, cs, cd, gs, ms, h, w);
     PG_UNROLL
     for (int j = 0; j < Q; j++) {
-        if (!run[j]) continue;
-        const uint32_t a = w[j] >> 30;
-        if (a == kActFailure || a == kActDeny) {
-            out[j] = verdict(a == kActFailure ? 3u : 0u, w[j] & kSlotMask);
-            live[j] = false;
-        } else if (a == kActReflect) {
-            srefl[j] = true;
-            drefl[j] = same[j];
-        }
+        const bool stop = run[j] && conn_stop(w[j]), refl = run[j] && (w[j] >> 30) == kActReflect;
+        if (stop) out[j] = w[j];
+        live[j] = live[j] && !stop;
+        srefl[j] = refl;
+        drefl[j] = refl && same[j];
     }
     // SYN: dst interface outbound
     PG_UNROLL
@@ -1116,15 +1134,11 @@ PG_HD void conn_uni_q(const DevTableSet& T, const DevNode& N, const L& img, cons
     uni_eval<Q, COUNT, CM, WIDE>(T, N, img, t, run, cs, cd, gs, ms, h, w);
     PG_UNROLL
     for (int j = 0; j < Q; j++) {
-        if (!run[j]) continue;
-        const uint32_t a = w[j] >> 30;
-        if (a == kActFailure || a == kActDeny) {
-            out[j] = verdict(a == kActFailure ? 3u : 0u, w[j] & kSlotMask);
-            live[j] = false;
-        } else if (a == kActReflect) {
-            drefl[j] = true;
-            if (same[j]) srefl[j] = true;
-        }
+        const bool stop = run[j] && conn_stop(w[j]), refl = run[j] && (w[j] >> 30) == kActReflect;
+        if (stop) out[j] = w[j];
+        live[j] = live[j] && !stop;
+        drefl[j] = drefl[j] || refl;
+        srefl[j] = srefl[j] || (refl && same[j]);
     }
     // SYN-ACK: dst interface inbound (reversed packet: the rule's src side is the dst class, the
     // SYN-ACK key's class)
@@ -1133,24 +1147,17 @@ PG_HD void conn_uni_q(const DevTableSet& T, const DevNode& N, const L& img, cons
     uni_eval<Q, COUNT, CM, WIDE>(T, N, img, t, run, cd, cs, ga, md, h, w);
     PG_UNROLL
     for (int j = 0; j < Q; j++) {
-        if (!run[j]) continue;
-        const uint32_t a = w[j] >> 30;
-        if (a == kActFailure || a == kActDeny) {
-            out[j] = verdict(a == kActFailure ? 3u : 1u, w[j] & kSlotMask);
-            live[j] = false;
-        }
+        const bool stop = run[j] && conn_stop(w[j]);
+        if (stop) out[j] = w[j] | 1u << 30;
+        live[j] = live[j] && !stop;
     }
     // SYN-ACK: src interface outbound
     PG_UNROLL
     for (int j = 0; j < Q; j++) t[j] = tso[j], run[j] = live[j] && !srefl[j];
     uni_eval<Q, COUNT, CM, WIDE>(T, N, img, t, run, cd, cs, ga, md, h, w);
     PG_UNROLL
-    for (int j = 0; j < Q; j++) {
-        if (!live[j]) continue;
-        const uint32_t a = w[j] >> 30;
-        if (run[j] && (a == kActFailure || a == kActDeny)) out[j] = verdict(a == kActFailure ? 3u : 1u, w[j] & kSlotMask);
-        else out[j] = verdict(2u, w[j] & kSlotMask);  // allowed; slot of the last evaluation
-    }
+    for (int j = 0; j < Q; j++)  // allowed: the slot of the last evaluation
+        if (live[j]) out[j] = run[j] && conn_stop(w[j]) ? w[j] | 1u << 30 : (w[j] & kSlotMask) | 2u << 30;
 }
 
 // evalACL of ANY-protocol packets (the L4 test skipped, aclengine_mock.go:562): the first rule

@@ -585,6 +585,9 @@ __device__ __forceinline__ void st_words(const Words<NW>& v, uint32_t* p) {
 #ifndef PG_NODE_WIDE_BS  // workgroup size of the wide node builds (node_wide)
 #define PG_NODE_WIDE_BS 1024
 #endif
+#ifndef PG_NODE_WIDE_REC_BS  // ... and of the other builds over wide class records (STAGE + 128)
+#define PG_NODE_WIDE_REC_BS 768
+#endif
 // node builds at 64 registers (wpe 8): 1024-thread workgroups and no stream prefetch (its
 // registers): CONN, and PERPOD counting into an LDS histogram of every slot (image + histogram
 // leave LDS for two workgroups per CU: 16 waves at 512 threads, 32 at 1024; A/B on MI355X,
@@ -1227,8 +1230,11 @@ static void launch_one(const DevTableSet& T, const Tuning& tu, int t, const uint
         const size_t lds_bytes = hist + (size_t)stage * 4;
         // (wide-record node builds, STAGE + 128: the per-mode workgroup size only -- block_stage is
         // an A/B knob of the other builds, and every extra size is another set of kernels)
+        // The wide sets' images are larger (config 9: 502 tables, 53.8 KB with the common rows),
+        // so LDS holds two workgroups per CU where config 3's 41 KB holds three: 768-thread
+        // workgroups keep the 24 waves per CU of three 512-thread ones (PG_NODE_WIDE_REC_BS)
         if constexpr (NODE && (STAGE & 128)) {
-            constexpr int BSW = node_wide<MODE, COUNT, NODE, STAGE>() ? PG_NODE_WIDE_BS : 512;
+            constexpr int BSW = node_wide<MODE, COUNT, NODE, STAGE>() ? PG_NODE_WIDE_BS : PG_NODE_WIDE_REC_BS;
             return launch_bs<MODE, COUNT, VEC, STAGE, NODE, BSW>(T, tu, t, src, dst, sport, dport, proto, n, out,
                                                                  counters, st, hist, cells, stage, items);
         }
