@@ -678,12 +678,12 @@ PG_HD End node_end(const L& img, const DevNode& N, uint32_t ipc) {
     const uint32_t tin = v.y & 0xFFFFu, tout = v.y >> 16;
     return End{(int32_t)v.x, tin == 0xFFFFu ? -1 : (int32_t)tin, tout == 0xFFFFu ? -1 : (int32_t)tout};
 }
-// packed end point (uniform layout: at most 254 tables): interface index (14 bits) | end-point kind
-// << 14 (0xFFFF: unresolved) | tin << 16 | tout << 24 (0xFF = no ACL)
-PG_HD End node_end_packed(uint32_t p) {
+// packed end point (uniform layout, narrow records): interface index (14 bits) | end-point kind
+// << 14 (0xFFFF: unresolved) | tin << 16 | tout << 24 (tnil = no ACL, DevNode tnil)
+PG_HD End node_end_packed(uint32_t p, uint32_t tnil) {
     const uint32_t f = p & 0xFFFFu, tin = (p >> 16) & 0xFFu, tout = p >> 24;
-    return End{f == 0xFFFFu ? -1 : (int32_t)((f & 0x3FFFu) | ((f >> 14) << kEndKindShift)), tin == 0xFFu ? -1 : (int32_t)tin,
-               tout == 0xFFu ? -1 : (int32_t)tout};
+    return End{f == 0xFFFFu ? -1 : (int32_t)((f & 0x3FFFu) | ((f >> 14) << kEndKindShift)), tin == tnil ? -1 : (int32_t)tin,
+               tout == tnil ? -1 : (int32_t)tout};
 }
 
 // wide class records (DevNode wide: 255 tables or more): interface index | kind << 14 (0xFFFF:
@@ -1028,17 +1028,20 @@ PG_HD void conn_q(const DevTableSet& T, const EV& ev, const End (&es)[Q], const 
 // is set, else from the cross array; a list resolves through the list-verdict table at the
 // rule-dst-side class cb. Counted (run lanes) into h. Key classes of valid keys only (the
 // callers leave ANY-protocol packets out of `run`).
+// "No ACL" (DevNode tnil): with the common-row section staged (CM) a narrow record's pseudo-table
+// reads its row of PERMIT words like any common row, so only wide records and launches without the
+// section test the id.
 template <int Q, bool COUNT, bool CM, bool WIDE, class L, class HS>
 PG_HD void uni_eval(const DevTableSet& T, const DevNode& N, const L& img, const uint32_t (&t)[Q], const bool (&run)[Q],
                     const uint32_t (&ca)[Q], const uint32_t (&cb)[Q], const uint32_t (&g)[Q], const W2 (&m)[Q],
                     const HS& h, uint32_t (&w)[Q]) {
-    constexpr uint32_t NIL = WIDE ? 0xFFFFu : 0xFFu;
+    constexpr bool NILROW = CM && !WIDE;
     const DevLoader X{N.cross};
     bool on[Q], cm[Q];
     uint32_t pos[Q];
     PG_UNROLL
     for (int j = 0; j < Q; j++) {
-        on[j] = run[j] && t[j] != NIL;
+        on[j] = run[j] && (NILROW || t[j] != N.tnil);
         uint32_t cw = 0;
         if (CM) {  // bit t >> gshift of the class's marks (wide records: one 32-bit word)
             const uint32_t tb = t[j] >> N.gshift;
@@ -1049,7 +1052,7 @@ PG_HD void uni_eval(const DevTableSet& T, const DevNode& N, const L& img, const 
         const uint32_t pc = mad24(t[j], N.gk, N.crow0 + g[j]);
         const uint32_t px = mad24(t[j], N.tstride, mad24(ca[j], N.gk, g[j]));
         pos[j] = cm[j] ? pc : px;
-        if (run[j] && !on[j]) w[j] = verdict(kActPermit, T.slot_noacl);  // nil ACL
+        if (!NILROW && run[j] && !on[j]) w[j] = verdict(kActPermit, T.slot_noacl);  // nil ACL
     }
     PG_UNROLL
     for (int j = 0; j < Q; j++)
@@ -1077,7 +1080,7 @@ PG_HD bool conn_stop(uint32_t w) { return (w + 0x40000000u) < 0x80000000u; }
 // the records' packed end points as they are instead of decoded End structs -- the kinds of the
 // two interfaces add to 3 or more exactly when the pair has no Connection* call or an interface
 // is unresolved (0xFFFF has kind 3), "same interface" is equality of the 16-bit interface
-// fields, and a table id equal to NIL (0xFF; wide records 0xFFFF) is "no ACL". Every
+// fields, and a table id equal to DevNode tnil is "no ACL". Every
 // evaluation computes its cross-entry address from (table, IP class, key class) and reads it
 // from the image when the class's common-row mark is set, else from the cross array; lists
 // resolve through the list-verdict table. (Two schedules that ran the SYN-ACK half elsewhere --
@@ -1360,7 +1363,6 @@ PG_HD void classify_node_q(const DevTableSet& T, const DevNode& N, const L& img,
         return;
     }
     if constexpr (MODE == 1 && UNI && PG_POD_UNI) {  // PERPOD: the dst record's outbound table as it is
-        constexpr uint32_t NIL = WIDE ? 0xFFFFu : 0xFFu;
         uint32_t t[Q];
         bool run[Q], fbk[Q];
         W2 ms[Q];
@@ -1376,7 +1378,7 @@ PG_HD void classify_node_q(const DevTableSet& T, const DevNode& N, const L& img,
                 if (COUNT && !df) h.inc_cold(T.slot_unresolved);
             }
             // ANY-protocol packets (no key class) on a table: the per-table path below
-            fbk[j] = run[j] && key[j] >= kWalkKeyLimit && t[j] != NIL;
+            fbk[j] = run[j] && key[j] >= kWalkKeyLimit && t[j] != N.tnil;
             run[j] = run[j] && !fbk[j];
         }
         uni_eval<Q, COUNT, CM, WIDE>(T, N, img, t, run, cs, cd, gs, ms, h, out);
@@ -1411,10 +1413,10 @@ PG_HD void classify_node_q(const DevTableSet& T, const DevNode& N, const L& img,
         } else if constexpr (UNI) {  // record {self, packed end point, mask lo, mask hi}
             if (MODE == 2) {
                 const W4 rs = img.u4_at_byte(rec[j]), rd = img.u4_at_byte(rec[Q + j]);
-                es[j] = node_end_packed(rs.y), ed[j] = node_end_packed(rd.y);
+                es[j] = node_end_packed(rs.y, N.tnil), ed[j] = node_end_packed(rd.y, N.tnil);
                 mks[j] = W2{rs.z, rs.w}, mkd[j] = W2{rd.z, rd.w};
             } else {
-                ed[j] = node_end_packed(img.at_byte(rec[Q + j] + 4u));
+                ed[j] = node_end_packed(img.at_byte(rec[Q + j] + 4u), N.tnil);
                 mks[j] = CM ? img.u2_at_byte(rec[j] + 8u) : W2{0u, 0u};
                 mkd[j] = mks[j];
             }

@@ -108,6 +108,10 @@ struct DevNode {
     // no ACL)} instead of {self, interface | kind << 14 | tin << 16 | tout << 24 (0xFF = no ACL),
     // marks lo, marks hi} (classify.hpp node_end_packed / node_end_wide)
     uint32_t wide;
+    // uniform layout: the table id of "no ACL" in the class records -- narrow records: a pseudo-table
+    // past the tables (T rounded up to 2^gshift) whose common row is PERMIT with the "no ACL" slot and
+    // whose mark every class has (fastpath.cpp build_node / build_common_rows); wide: 0xFFFF
+    uint32_t tnil;
     // list-verdict table (Tuning::node_list_table; 0 = the record form above): a kNodeList word's
     // low bits are a list id L, and its verdict for the rule's dst-side address is cross word
     // lv0 + L * n_ipc + (that address's node IP class) -- one gather, no record walk

@@ -947,10 +947,15 @@ void build_common_rows(HostTableSet& h, const std::vector<uint32_t>& cov, const 
     // 64 tables a bit covers a group of 2^gshift consecutive tables (bit t >> gshift): set when the
     // class's row is the common one in every table of the group, so an evaluation whose group bit
     // is clear gathers its entry from the cross table, which holds every row
-    // (wide records, DevNode wide: one 32-bit mark word, so T <= 32 << gshift)
+    // (wide records, DevNode wide: one 32-bit mark word, so T <= 32 << gshift); the uniform
+    // layout's "no ACL" pseudo-table tnil (build_node) takes the group after the tables
     const uint32_t mbits = N.wide ? 32u : 64u;
     uint32_t gshift = 0;
     while (uni && (mbits << gshift) < T) gshift++;
+    if (uni && !N.wide)
+        while ((N.tnil >> gshift) >= mbits) gshift++;
+    // (the pseudo-table's group must hold no table: tnil a multiple of 2^gshift, past T)
+    if (uni && !N.wide && (N.tnil < T || (N.tnil & ((1u << gshift) - 1u)) != 0)) return;
     N.gshift = gshift;
     std::vector<uint32_t> masks(uni ? 2 * (size_t)G : 0, 0);
     std::vector<uint8_t> grp_common(uni ? (size_t)G * 64 : 0, 1);  // [g][group]: every table common
@@ -983,6 +988,15 @@ void build_common_rows(HostTableSet& h, const std::vector<uint32_t>& cov, const 
         for (uint32_t g = 0; g < G; g++)
             for (uint32_t b = 0; b < mbits && (b << gshift) < T; b++)
                 if (grp_common[(size_t)g * 64 + b]) masks[2 * (size_t)g + (b >> 5)] |= 1u << (b & 31u);
+    if (uni && !N.wide) {  // rows up to tnil (unused ones zero), then tnil's: PERMIT, the "no ACL" slot
+        const uint32_t noacl = (uint32_t)h.rules.size() + T;
+        sec.resize((size_t)N.tnil * N.gk, 0u);
+        sec.insert(sec.end(), N.gk, (kActPermit << 30) | noacl);
+        for (uint32_t g = 0; g < G; g++) {
+            const uint32_t b = N.tnil >> gshift;
+            masks[2 * (size_t)g + (b >> 5)] |= 1u << (b & 31u);
+        }
+    }
     while (sec.size() % 4) sec.push_back(0);
     const uint32_t s0 = (uint32_t)img.size();
     for (uint32_t t : cov) TI[N.tabinfo + 4 * t + 2] = s0 + crow[t];
@@ -1157,7 +1171,22 @@ bool build_node(HostTableSet& h, const std::vector<TableAnalysis*>& an, const st
     bool pack_ok = true;
     for (const auto& k : ipc_key)
         if ((int32_t)k[0] >= 0 && (k[0] & ~(3u << kEndKindShift)) >= 0x4000u) pack_ok = false;
-    const bool wide = T >= 255;  // (build_node: T < 0xFFFF, so 0xFFFF stays "no ACL")
+    // "no ACL" is a pseudo-table id tnil: the first id of a group of common-row marks past the
+    // tables (T rounded up to 2^gshift), whose common row holds PERMIT with the "no ACL" slot in
+    // every column and whose mark is set in every class (build_common_rows), so an evaluation of
+    // it reads that row like any common row -- no test of the id in the kernels that stage the
+    // section (classify.hpp uni_eval). Narrow records need tnil below 255.
+    auto gshift_for = [](uint32_t tabs, uint32_t mbits) {
+        uint32_t g = 0;
+        while (((((tabs + (1u << g) - 1u) >> g) << g) >> g) >= mbits) g++;  // tnil's group index < mbits
+        return g;
+    };
+    // Wide records keep 0xFFFF for "no ACL", tested in their kernels (their 32-bit marks have no
+    // group to spare).
+    const uint32_t gs_nil = gshift_for(T, 64);
+    const uint32_t tnil_narrow = ((T + (1u << gs_nil) - 1u) >> gs_nil) << gs_nil;
+    const bool wide = tnil_narrow >= 255;  // (build_node: T < 0xFFFF)
+    const uint32_t tnil = wide ? 0xFFFFu : tnil_narrow;
     // uniform layout (DevNode uniform): every table covered, none in PAIR form -- rows over the
     // node key classes at cross[(t * G + ip class) * GK + key class], so an evaluation computes
     // its entry's address from (t, classes) instead of reading tabinfo and kmap (at most 64
@@ -1289,8 +1318,8 @@ bool build_node(HostTableSet& h, const std::vector<TableAnalysis*>& an, const st
         uint32_t* r = img.data() + irec0 + rw * (size_t)g;
         r[0] = node_entry(irec0 + rw * g, 0u, aligned);
         if (aligned) {
-            auto t8 = [](uint32_t t) { return (int32_t)t < 0 ? 0xFFu : t; };
-            auto t16 = [](uint32_t t) { return (int32_t)t < 0 ? 0xFFFFu : t; };
+            auto t8 = [&](uint32_t t) { return (int32_t)t < 0 ? tnil : t; };
+            auto t16 = [&](uint32_t t) { return (int32_t)t < 0 ? tnil : t; };
             const uint32_t f = (int32_t)k[0] < 0 ? 0xFFFFu : ((k[0] & 0x3FFFu) | ((k[0] >> kEndKindShift) & 3u) << 14);
             if (wide) {
                 r[1] = f;
@@ -1336,6 +1365,7 @@ bool build_node(HostTableSet& h, const std::vector<TableAnalysis*>& an, const st
     N.n_ipc = G;
     N.n_pair = (uint32_t)PC;
     N.wide = aligned && wide;
+    N.tnil = aligned ? tnil : 0xFFFFFFFFu;
     N.img_words = N.img_words_base = (uint32_t)img.size();
     N.cmap = 0;
 
