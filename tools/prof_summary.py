@@ -76,14 +76,16 @@ def main():
                              os.path.join(prof, f"{prefix}_config{cfg}_kernel_stats.csv"))
         fetch = pmc_values(os.path.join(src, f"pmc_FETCH_SIZE_c{cfg}"), "FETCH_SIZE")
         write = pmc_values(os.path.join(src, f"pmc_WRITE_SIZE_c{cfg}"), "WRITE_SIZE")
-        kname = next(k for k in fetch if "k_classify" in k)
+        # the config's own kernel: the k_classify launched most often (the default config-2 line
+        # also times its side blocks' kernels, fewer times each)
+        kname = max((k for k in fetch if "k_classify" in k), key=lambda k: len(fetch[k]))
         avg = lambda xs: sum(xs) / len(xs)
         f_raw = avg(fetch[kname]) * 1024
         w_raw = avg(write[kname]) * 1024
         n = line["config"]["tuples_per_gpu"]
         stream_read = n * (line["roofline"]["bytes_per_tuple"] - 4)
         algo = n * line["roofline"]["bytes_per_tuple"]
-        prof_avg_ns = next(float(s["AverageNs"]) for s in stats if "k_classify" in s["Name"])
+        prof_avg_ns = next(float(s["AverageNs"]) for s in stats if s["Name"] == kname)
         # the tuple streams show up at half their bytes; whatever FETCH_SIZE holds beyond
         # that is table-blob (L2-miss) reads, taken at face value (uncalibrated width)
         stream_raw = min(f_raw, stream_read / 2)
