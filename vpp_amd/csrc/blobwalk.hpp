@@ -93,6 +93,9 @@ PG_HD constexpr uint32_t blob_root_words(uint32_t fsk, uint32_t nkc) {
     return (((fsk & kFlagCandI) && nkc ? candi_window_off((fsk >> 8) & 0xFFu) + 2u * nkc
                                        : kSrcRoot + (1u << ((fsk >> 8) & 0xFFu))) + 3u) & ~3u;
 }
+// the largest table array (a table's blob, the node image, the node cross array) a DevLoader
+// reads: its byte offsets are 32-bit (classify.hpp)
+constexpr uint64_t kMaxLoaderBytes = 1ull << 32;
 constexpr uint32_t kWalkKeyLimit = 0x30000u;  // keys >= this (ANY protocol) take the linear path
 // key bound of records that match every key: covers the whole 18-bit walk range, ANY keys
 // included, so every list terminates for any key the walk is given

@@ -101,16 +101,21 @@ PG_NOINLINE uint32_t eval_linear(const DevRule* rules, uint32_t base, uint32_t n
 }
 
 // 16/8/4-byte loads from LDS or global memory (the device infers the address space).
+// Loads from a table array in global memory by 32-bit BYTE offsets (every array a loader reads
+// is below kMaxLoaderBytes, checked where the arrays are built): the device load is then the
+// array's SGPR base plus a 32-bit VGPR offset, with no 64-bit address arithmetic per gather.
 struct DevLoader {
     const uint32_t* b;
-    PG_HD uint32_t u32(uint32_t i) const { return b[i]; }
-    PG_HD uint32_t at_byte(uint32_t off) const {
-        return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(b) + off);
+    template <class V>
+    PG_HD const V& ref(uint32_t off) const {
+        return *reinterpret_cast<const V*>(reinterpret_cast<const char*>(b) + off);
     }
-    PG_HD uint32_t u16(uint32_t i) const { return reinterpret_cast<const uint16_t*>(b)[i]; }  // halfword i
+    PG_HD uint32_t u32(uint32_t i) const { return ref<uint32_t>(i * 4u); }
+    PG_HD uint32_t at_byte(uint32_t off) const { return ref<uint32_t>(off); }
+    PG_HD uint32_t u16(uint32_t i) const { return ref<uint16_t>(i * 2u); }  // halfword i
     PG_HD W2 u2(uint32_t i) const {
 #if defined(__HIP_DEVICE_COMPILE__)
-        const uint2 v = *reinterpret_cast<const uint2*>(b + i);
+        const uint2 v = ref<uint2>(i * 4u);
         return W2{v.x, v.y};
 #else
         return W2{b[i], b[i + 1]};
@@ -118,7 +123,7 @@ struct DevLoader {
     }
     PG_HD W4 u4(uint32_t i) const {
 #if defined(__HIP_DEVICE_COMPILE__)
-        const uint4 v = *reinterpret_cast<const uint4*>(b + i);
+        const uint4 v = ref<uint4>(i * 4u);
         return W4{v.x, v.y, v.z, v.w};
 #else
         return W4{b[i], b[i + 1], b[i + 2], b[i + 3]};
@@ -1045,7 +1050,7 @@ PG_HD void uni_eval(const DevTableSet& T, const DevNode& N, const L& img, const 
         uint32_t cw = 0;
         if (CM) {  // bit t >> gshift of the class's marks (wide records: one 32-bit word)
             const uint32_t tb = t[j] >> N.gshift;
-            cw = WIDE ? bit_of(m[j].x, tb) : bit_of(tb < 32u ? m[j].x : m[j].y, tb);
+            cw = WIDE ? bit_of(m[j].x, tb) : (uint32_t)((((uint64_t)m[j].y << 32) | m[j].x) >> (tb & 63u)) & 1u;
         }
         cm[j] = CM && cw != 0u;
         // the common row's entry in the image, or the cross entry t * tstride + class * GK + k
@@ -1287,6 +1292,18 @@ PG_HD void classify_node_q(const DevTableSet& T, const DevNode& N, const L& img,
     uint32_t key[Q], kack[Q];
     PG_UNROLL
     for (int j = 0; j < Q; j++) key[j] = pkt_key(pr[j], dp[j]), kack[j] = MODE == 2 ? pkt_key(pr[j], sp[j]) : key[j];
+    // CONN over a uniform node, ANY-protocol packets deferred: the keys of the other protocols
+    // as pkt_key gives them, and for a deferred packet any key below 2^18 (its walks' results are
+    // not used) -- so the keys need no clamp before the walks
+    constexpr bool KEYS18 = MODE == 2 && UNI && DEFER && PG_CONN_UNI;
+    if constexpr (KEYS18) {
+        PG_UNROLL
+        for (int j = 0; j < Q; j++) {
+            const uint32_t prm = (pr[j] & 3u) << 16, pm = pr[j] < 2u ? 0xFFFFu : 0u;
+            key[j] = prm | (dp[j] & pm);
+            kack[j] = prm | (sp[j] & pm);
+        }
+    }
     // node IP class records of src and dst, node key classes of both keys: 2Q + 2Q trie walks
     uint32_t ips[2 * Q], rec[2 * Q];
     PG_UNROLL
@@ -1297,8 +1314,8 @@ PG_HD void classify_node_q(const DevTableSet& T, const DevNode& N, const L& img,
         uint32_t keys[2 * Q], kc[2 * Q];
         PG_UNROLL
         for (int j = 0; j < Q; j++) {
-            keys[j] = key[j] < kWalkKeyLimit ? key[j] : 0u;
-            keys[Q + j] = kack[j] < kWalkKeyLimit ? kack[j] : 0u;
+            keys[j] = KEYS18 || key[j] < kWalkKeyLimit ? key[j] : 0u;
+            keys[Q + j] = KEYS18 || kack[j] < kWalkKeyLimit ? kack[j] : 0u;
         }
         node_walks<PRED, UNI>(img, N, ips, rec, keys, kc);
         PG_UNROLL
@@ -1356,7 +1373,7 @@ PG_HD void classify_node_q(const DevTableSet& T, const DevNode& N, const L& img,
         PG_UNROLL
         for (int j = 0; j < Q; j++) {
             rs[j] = img.u4_at_byte(rec[j]), rd[j] = img.u4_at_byte(rec[Q + j]);
-            dfr[j] = key[j] >= kWalkKeyLimit || kack[j] >= kWalkKeyLimit;
+            dfr[j] = pr[j] > 2u;  // (ANY protocol: both keys >= kWalkKeyLimit in pkt_key)
         }
         conn_uni_q<Q, COUNT, CM, WIDE>(T, N, img, rs, rd, cs, cd, gs, ga, dfr, h, out);
         hook();

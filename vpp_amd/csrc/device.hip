@@ -515,6 +515,13 @@ __global__ __launch_bounds__(kBlock) void k_node_any(DevTableSet T, const uint32
     for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride)
         if (proto[i] > 2u) out[i] = MODE == 2 ? conn_any_1<COUNT>(T, src[i], dst[i], h) : pod_any_1<COUNT>(T, src[i], dst[i], h);
 }
+#ifndef PG_IDX32  // k_classify's group indices and stream offsets in 32 bits (launches below kMaxLaunchTuples)
+#define PG_IDX32 1
+#endif
+// the most tuples one k_classify launch takes: every stream's byte offset below 2^32 (dev_classify
+// splits larger batches into launches of at most this many; a multiple of 64, so the pieces stay
+// vector-aligned)
+constexpr uint64_t kMaxLaunchTuples = PG_IDX32 ? (1ull << 30) - 64 : ~0ull;
 #ifndef PG_TPL  // tuples per lane per loop iteration (4 or 8)
 #define PG_TPL 4
 #endif
@@ -825,14 +832,24 @@ void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
         }
     }
     if (STAGE || COUNT) __syncthreads();
-    const uint64_t stride = (uint64_t)gridDim.x * BS;
-    const uint64_t first = (uint64_t)blockIdx.x * BS + threadIdx.x;
+    // group indices and stream offsets in 32 bits (PG_IDX32: the launcher keeps a launch below
+    // kMaxLaunchTuples, so every byte offset of a stream fits 32 bits): a load is then the SGPR base
+    // plus a 32-bit VGPR offset, with no 64-bit address arithmetic per stream and group
+    using Idx = std::conditional_t<PG_IDX32 != 0, uint32_t, uint64_t>;
+    const Idx stride = (Idx)gridDim.x * BS;
+    const Idx first = (Idx)blockIdx.x * BS + threadIdx.x;
     // full groups of P tuples per lane (P = tuples_per_lane): SoA fields read with 16/8/4-byte loads per
     // lane (coalesced, non-temporal); prefetch 1/2: the next group's loads are in flight
     // while this group is classified
     constexpr int P = tuples_per_lane<MODE>();
     static_assert(P % 4 == 0, "a group's protocol bytes are loaded as whole words (PG_TPL, PG_TPL_CONN)");
-    const uint64_t nfull = VEC ? (n / P) : 0;
+    const Idx nfull = VEC ? (Idx)(n / P) : 0;
+    // element i of a stream, its byte offset computed in Idx
+    auto el = [](auto* base, Idx i) {
+        using E = std::remove_pointer_t<decltype(base)>;
+        using C = std::conditional_t<std::is_const<E>::value, const char, char>;
+        return reinterpret_cast<decltype(base)>(reinterpret_cast<C*>(base) + (Idx)(i * (Idx)sizeof(E)));
+    };
     struct Group {
         Words<P> s, d;
         Words<P / 2> dp, sp;
@@ -842,19 +859,19 @@ void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
     constexpr bool FD = MODE == 0 && (STAGE == 4 || STAGE == 5);
     constexpr bool NEED_DST = !FD && !NODST;
     const uint32_t* fd_blob = FD ? (STAGE == 4 ? smem : T.blobs + tab0.blob_off) : nullptr;
-    auto load = [&](uint64_t q) {
+    auto load = [&](Idx q) {
         Group x;
-        const uint64_t i0 = q * P;
-        x.s = ld_words<P>(src + i0);
-        if (NEED_DST) x.d = ld_words<P>(dst + i0);
+        const Idx i0 = q * P;
+        x.s = ld_words<P>(el(src, i0));
+        if (NEED_DST) x.d = ld_words<P>(el(dst, i0));
         else x.d = Words<P>{};
-        x.dp = ld_words<P / 2>(reinterpret_cast<const uint32_t*>(dport + i0));
-        x.pr = ld_words<P / 4>(reinterpret_cast<const uint32_t*>(proto + i0));
-        if (MODE == 2) x.sp = ld_words<P / 2>(reinterpret_cast<const uint32_t*>(sport + i0));
+        x.dp = ld_words<P / 2>(reinterpret_cast<const uint32_t*>(el(dport, i0)));
+        x.pr = ld_words<P / 4>(reinterpret_cast<const uint32_t*>(el(proto, i0)));
+        if (MODE == 2) x.sp = ld_words<P / 2>(reinterpret_cast<const uint32_t*>(el(sport, i0)));
         else x.sp = Words<P / 2>{};
         return x;
     };
-    uint64_t q = first;
+    Idx q = first;
     Group cur;
     // default: SINGLE over an LDS-staged blob none, SINGLE over a blob in HBM (STAGE 0 / 2) and
     // the node modes the next group at the top of the iteration (A/B on MI355X, config 4 with
@@ -873,7 +890,7 @@ void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
     constexpr int PD = PF ? PG_PF_DEPTH : 1;
     // classification of one group (P tuples per lane, loaded), its verdicts stored; hk: called
     // once after the first chunk's cross-entry loads are issued (node kernels, PF 2)
-    auto run_group = [&](const Group& g, uint64_t qq, auto&& hk) {
+    auto run_group = [&](const Group& g, Idx qq, auto&& hk) {
         uint32_t sv[P], dv[P], spv[P], dpv[P], prv[P], o[P];
         // (DEFER) a protocol code > 2 among the group's: this launch's number into its stream's
         // mark word for k_node_any (one test of the packed protocol word per group, no state
@@ -932,13 +949,13 @@ void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
         Words<P> ow;
 #pragma unroll
         for (int j = 0; j < P; j++) ow.w[j] = o[j];
-        st_words<P>(ow, out + qq * P);
+        st_words<P>(ow, el(out, qq * P));
     };
     Group ahead{};
     if (PF && q < nfull) cur = load(q);
     if (PD == 2 && q + stride < nfull) ahead = load(q + stride);
     while (q < nfull) {
-        const uint64_t qn = q + stride, qa = PD == 2 ? qn + stride : qn;  // qa: the group loaded now
+        const Idx qn = q + stride, qa = PD == 2 ? qn + stride : qn;  // qa: the group loaded now
         Group nxt = PD == 2 ? ahead : cur;
         if (!PF) cur = load(q);
         auto issue = [&]() {
@@ -957,7 +974,7 @@ void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
         q = qn;
     }
     // remainder (or everything when the pointers are not vector-aligned): one tuple per lane
-    for (uint64_t i = nfull * P + first; i < n; i += stride) {
+    for (uint64_t i = (uint64_t)nfull * P + first; i < n; i += stride) {
         const uint32_t s1[1] = {src[i]}, d1[1] = {NEED_DST ? dst[i] : 0u},
                        sp1[1] = {MODE == 2 ? (uint32_t)sport[i] : 0u}, dp1[1] = {dport[i]}, pr1[1] = {proto[i]};
         uint32_t o[1];
@@ -1401,6 +1418,15 @@ int dev_classify(const DevTableSet& T, const Tuning& tu, int mode, int table_id,
                  const uint32_t* dst, const uint16_t* sport, const uint16_t* dport, const uint8_t* proto, uint64_t n,
                  uint32_t* out, unsigned long long* counters, void* stream, std::string* err) {
     if (n == 0) return 0;
+    if (n > kMaxLaunchTuples) {  // (PG_IDX32) pieces of at most kMaxLaunchTuples, in order on the stream
+        for (uint64_t o = 0; o < n; o += kMaxLaunchTuples) {
+            const uint64_t k = std::min<uint64_t>(kMaxLaunchTuples, n - o);
+            const int rc = dev_classify(T, tu, mode, table_id, src + o, dst + o, sport ? sport + o : nullptr, dport + o,
+                                        proto + o, k, out + o, counters, stream, err);
+            if (rc != 0) return rc;
+        }
+        return 0;
+    }
     if (mode != 0 && !T.any_mark) {  // (a node build may defer packets to k_node_any: dev_any_mark)
         if (err) *err = "PERPOD / CONN launch without a launch-mark word";
         return -1;

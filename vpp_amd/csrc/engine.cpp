@@ -410,6 +410,7 @@ void Engine::compile() {
                 h.blob_prefix[t] = blob[9];
             }
         }
+        ok = ok && (uint64_t)blob.size() * 4u < kMaxLoaderBytes;  // (the loaders' 32-bit byte offsets)
         if (ok) {
             while (blob.size() % 4) blob.push_back(0);
             hdr.blob_off = (uint32_t)h.blobs.size();

@@ -1486,6 +1486,14 @@ bool build_node(HostTableSet& h, const std::vector<TableAnalysis*>& an, const st
         N.img_words = (uint32_t)img.size();
     }
     if (X.empty()) X.resize(4, 0);
+    if ((uint64_t)X.size() * 4u >= kMaxLoaderBytes || (uint64_t)img.size() * 4u >= kMaxLoaderBytes) {
+        h.node_img.clear();  // (the loaders' 32-bit byte offsets: no node; the per-table path)
+        h.node_aux.clear();
+        h.node_cross.clear();
+        h.node = DevNode{};
+        h.node_rec_words = 0;
+        return false;
+    }
     if (std::getenv("PG_NODE_DEBUG"))  // measurement aid: the image's shape
         std::fprintf(stderr,
                      "node: T %u G %u GK %u uniform %u | ip root %u depth %u, key root %u depth %u | words: "
