@@ -183,7 +183,9 @@ int pg_ctx_device(const pg_ctx* ctx);
  * (record form: node dst records up to this many words go into the node image, so a launch that
  * stages the image walks them in LDS; default 4096, 0 = never), "pair" (1/0: the PAIR structure -- src x dst classes, then x key classes
  * -- for tables the cross product cannot take, default 1; 0 = candidate lists; 2 = wherever it
- * fits, for tests).
+ * fits, for tests), "launch_max_tuples" (a pg_classify batch larger than this takes several
+ * kernel launches of at most this many tuples, in order on the stream; a multiple of 64, 0 =
+ * the largest a launch's 32-bit stream offsets allow, 2^30 - 64; default 0).
  * pg_ctx_set_tuning sets one context's knob; pg_set_tuning sets the process default that
  * contexts created afterwards start from. PG_EINVAL for an unknown key or a value out of range. */
 int pg_ctx_set_tuning(pg_ctx* ctx, const char* key, int value);

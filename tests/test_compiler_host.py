@@ -287,3 +287,18 @@ def test_config2_table_is_fd():
     w = W.config2(0, n_tuples=1 << 10)
     st = w.engine.table_stats(w.table_id)
     assert st["structure"] == "fd" and st["blob_bytes"] <= 64 << 10 and st["key_classes"] == 21, st
+
+
+def test_launch_max_tuples_knob():
+    """Tuning launch_max_tuples (device.hip dev_classify: the most tuples one k_classify launch
+    takes; 0 = the 32-bit stream offsets' limit, 2^30 - 64): multiples of 64 up to that limit,
+    anything else PG_EINVAL; a context's value reads back."""
+    e = R.Engine(0)
+    assert e.get_tuning("launch_max_tuples") == 0
+    for v in (64, 64 * 1001, (1 << 30) - 64, 0):
+        e.set_tuning("launch_max_tuples", v)
+        assert e.get_tuning("launch_max_tuples") == v
+    for v in (1, 63, 65, 1 << 30, -64):
+        with pytest.raises(Exception):
+            e.set_tuning("launch_max_tuples", v)
+    assert e.get_tuning("launch_max_tuples") == 0

@@ -383,6 +383,32 @@ def test_conn_any_protocol_concurrent_streams():
             assert ((got >> 30) == expect[k].astype(np.uint32)).all(), (order, k)
 
 
+@pytest.mark.parametrize("config", [2, 3, 4, 5])
+def test_launch_split_equals_one_launch(config):
+    """A batch classified in several launches gives the verdicts and hit counters of one launch:
+    Tuning launch_max_tuples = 64 x 1001 over a ragged batch (dev_classify splits a batch above
+    2^30 - 64 tuples, the most a launch's 32-bit stream offsets allow, the same way), CONN with
+    ANY-protocol packets among the tuples (their deferred pass runs per launch)."""
+    from vpp_amd import workloads as W
+    w = W.CONFIGS[config](0, n_tuples=(1 << 20) + 37)
+    e = w.engine
+    b = D.TupleBatch(w.n_tuples, with_sport=True)
+    D.gen_tuples(e, b, **w.gen)
+    if w.mode == MODE_CONN:
+        b.proto[::97] = 7
+    res = []
+    for cap in (0, 64 * 1001):
+        with e.tuning(launch_max_tuples=cap):
+            out = torch.empty(b.n, dtype=torch.int32, device="cuda")
+            cnt = torch.zeros(e.num_counter_slots(), dtype=torch.int64, device="cuda")
+            D.classify(e, w.mode, w.table_id, b, out, counters=cnt)
+            torch.cuda.synchronize()
+            res.append((out.cpu().numpy(), cnt.cpu().numpy()))
+    assert np.array_equal(res[0][0], res[1][0])
+    assert np.array_equal(res[0][1], res[1][1])
+    assert int(res[0][1].sum()) >= b.n
+
+
 @pytest.mark.parametrize("mode", [MODE_PERPOD, MODE_CONN])
 def test_k8s_object_cluster_gpu_vs_oracle(mode):
     """The cluster given as K8s objects (policy cache -> processor -> configurator -> renderer,

@@ -1418,9 +1418,12 @@ int dev_classify(const DevTableSet& T, const Tuning& tu, int mode, int table_id,
                  const uint32_t* dst, const uint16_t* sport, const uint16_t* dport, const uint8_t* proto, uint64_t n,
                  uint32_t* out, unsigned long long* counters, void* stream, std::string* err) {
     if (n == 0) return 0;
-    if (n > kMaxLaunchTuples) {  // (PG_IDX32) pieces of at most kMaxLaunchTuples, in order on the stream
-        for (uint64_t o = 0; o < n; o += kMaxLaunchTuples) {
-            const uint64_t k = std::min<uint64_t>(kMaxLaunchTuples, n - o);
+    // (PG_IDX32) pieces of at most kMaxLaunchTuples (or Tuning launch_max_tuples), in order on the stream
+    const uint64_t cap = tu.launch_max_tuples ? std::min<uint64_t>(tu.launch_max_tuples, kMaxLaunchTuples)
+                                              : kMaxLaunchTuples;
+    if (n > cap) {
+        for (uint64_t o = 0; o < n; o += cap) {
+            const uint64_t k = std::min<uint64_t>(cap, n - o);
             const int rc = dev_classify(T, tu, mode, table_id, src + o, dst + o, sport ? sport + o : nullptr, dport + o,
                                         proto + o, k, out + o, counters, stream, err);
             if (rc != 0) return rc;

@@ -253,6 +253,7 @@ struct Tuning {
     uint32_t node_common_lds_max = 80u << 10;    // LDS bytes up to which the common-row section is staged
     uint32_t block_stage = 0;      // workgroup size of LDS-staged launches (0 = per mode)
     uint32_t hist_window = 4096;   // LDS hit-counter cells when the slots exceed the LDS histogram
+    uint32_t launch_max_tuples = 0;  // tuples per k_classify launch at most (0 = kMaxLaunchTuples)
 };
 // key -> field; 0 ok, -1 unknown key or value out of range. *compiler: the key changes how
 // tables are compiled (the context recompiles on its next use).

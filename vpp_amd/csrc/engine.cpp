@@ -69,10 +69,12 @@ const Knob kKnobs[] = {
     {"node_common_lds_max", &Tuning::node_common_lds_max, 0, 160 << 10, false},
     {"block_stage", &Tuning::block_stage, 0, 1024, false},
     {"hist_window", &Tuning::hist_window, 1, 16382, false},
+    {"launch_max_tuples", &Tuning::launch_max_tuples, 0, (1 << 30) - 64, false},
 };
 bool Knob::allowed(int v) const {
     if (field == &Tuning::lc_max_stride) return v == 12 || v == 16 || v == 18;
     if (field == &Tuning::block_stage) return v == 0 || v == 256 || v == 512 || v == 1024;
+    if (field == &Tuning::launch_max_tuples) return v % 64 == 0;  // (pieces stay vector-aligned)
     return true;
 }
 }  // namespace
