@@ -1,7 +1,7 @@
 #!/bin/bash
 # A/B of builds (tools/sweep.py in alternating processes) on the given configs, 2 rounds.
 # Builds: make -C vpp_amd/csrc variant V=name DEFS="-DPG_...=..." -> vpp_amd/libpolicygpu_name.so
-# Configs: 3, 5c (with counters), r10000 (config 2 at 10k rules), ...
+# Configs: 3, 5c (with counters), r10000 (config 2 at 10k rules), 9m2c (config 9 in mode 2, counted), ...
 #   gpurun -- bash tools/ab.sh TAG "libA libB" "3 5c 6" [pytest paths]
 # PRE="key=v ..." (environment): compiler knobs set before the tables are built (sweep.py --pre)
 # TUNE="key=v1,v2 ..." (environment): launch knobs swept inside each run (sweep.py --tune)
@@ -24,6 +24,7 @@ for lib in $LIBS; do
     for c in $CONFIGS; do
         cnt=""; case $c in *c) cnt="--counters";; esac
         extra=""; case $c in r*) extra="--rules ${c#r}"; c=2;; esac
+        case $c in *m*) b=${c%c}; extra="$extra --mode ${b#*m}"; c=${b%m*};; esac
         step sweep $lib config $c $cnt $extra
         pre=""; for kv in ${PRE:-}; do pre="$pre --pre $kv"; done
         for kv in ${TUNE:-}; do pre="$pre --tune $kv"; done

@@ -34,6 +34,7 @@ def main():
     ap.add_argument("--pre", action="append", default=[], help="key=v set before the tables are compiled")
     ap.add_argument("--ns", type=int, default=0, help="configs 3/5: namespaces (default 10)")
     ap.add_argument("--rules", type=int, default=0, help="config 2: rules of the gen-policy-shaped table")
+    ap.add_argument("--mode", type=int, default=-1, help="cluster configs: classify in this mode (2 = CONN)")
     a = ap.parse_args()
     kw = {"n_tuples": a.tuples} if a.tuples else {}
     if a.rules:
@@ -45,6 +46,8 @@ def main():
         assert _capi.lib.pg_set_tuning(k.encode(), int(v)) == 0, t
     w = W.CONFIGS[a.config](0, **kw)
     e, n = w.engine, w.n_tuples
+    if a.mode >= 0:
+        w.mode = a.mode
     b = D.TupleBatch(n, with_sport=(w.mode == 2))
     D.gen_tuples(e, b, **w.gen)
     keys, vals = [], []
@@ -83,7 +86,7 @@ def main():
     for i, combo in enumerate(combos):
         ms = float(np.median(times[i]))
         extra = {"blob": e.table_stats(w.table_id)} if w.mode == 0 and i == 0 else {}
-        print(json.dumps({"lib": name, "config": a.config, "counters": a.counters, "pre": a.pre, "ns": a.ns, "rules": a.rules, **dict(zip(keys, combo)), "ms": round(ms, 4),
+        print(json.dumps({"lib": name, "config": a.config if a.mode < 0 else "%dm%d" % (a.config, a.mode), "counters": a.counters, "pre": a.pre, "ns": a.ns, "rules": a.rules, **dict(zip(keys, combo)), "ms": round(ms, 4),
                           "gpps": round(n / ms / 1e6, 1), "GBps": round(n * bpt / ms / 1e6, 1),
                           "same_output": bool(torch.equal(outs[i], ref)),
                           "out_sha": __import__("hashlib").sha1(outs[i].cpu().numpy().tobytes()).hexdigest()[:12],
