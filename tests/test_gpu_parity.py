@@ -409,6 +409,42 @@ def test_launch_split_equals_one_launch(config):
     assert int(res[0][1].sum()) >= b.n
 
 
+def test_batch_past_32bit_stream_offsets():
+    """A batch of 2^30 + 4103 tuples (config 2's table, device-generated; ~19 GB of HBM): the
+    library splits it at 2^30 - 64 tuples, so the first launch reads its src stream up to byte
+    2^32 - 260 through 32-bit offsets (PG_IDX32). Its verdicts equal those of launches of 2^29
+    tuples (launch_max_tuples), and the tuples around the split and at the end equal the
+    oracle's."""
+    from oracle.world import expected
+    from vpp_amd import workloads as W
+    if torch.cuda.get_device_properties(0).total_memory < (64 << 30):
+        pytest.skip("needs a large-HBM GPU")
+    w = W.config2(0, n_tuples=1024)
+    e = w.engine
+    n = (1 << 30) + 4103
+    b = D.TupleBatch(n, with_sport=False)
+    D.gen_tuples(e, b, **w.gen)
+    outs = []
+    for cap in (0, 1 << 29):
+        with e.tuning(launch_max_tuples=cap):
+            out = torch.empty(n, dtype=torch.int32, device="cuda")
+            D.classify(e, w.mode, w.table_id, b, out)
+            torch.cuda.synchronize()
+            outs.append(out)
+    assert torch.equal(outs[0], outs[1])
+    split = (1 << 30) - 64
+    for lo, hi in ((split - 4096, split + 4096), (n - 8192, n)):
+        tup = tuple(x[lo:hi].cpu().numpy().view(dt) for x, dt in
+                    ((b.src, np.uint32), (b.dst, np.uint32), (b.dport, np.uint16), (b.proto, np.uint8)))
+        src, dst, dport, proto = tup
+        act, slot, _ = expected(e, w.mode, w.table_id, w.local_ifs, w.node_if, src, dst,
+                                np.zeros(hi - lo, np.uint16), dport, proto)
+        got = outs[0][lo:hi].cpu().numpy().view(np.uint32)
+        assert ((got >> 30) == act.astype(np.uint32)).all() and ((got & 0x3FFFFFFF) == slot).all()
+    del outs, b
+    torch.cuda.empty_cache()
+
+
 @pytest.mark.parametrize("mode", [MODE_PERPOD, MODE_CONN])
 def test_k8s_object_cluster_gpu_vs_oracle(mode):
     """The cluster given as K8s objects (policy cache -> processor -> configurator -> renderer,
