@@ -235,6 +235,56 @@ def test_config9_more_than_254_tables_wide_records():
     assert len(set((got >> 30).tolist())) >= 3
 
 
+def _many_tables(n_tables, seed):
+    """n_tables - 1 local pods, each with its own small outbound ACL, and a global ACL on the
+    node-output interface: n_tables tables, every one covered by the node."""
+    rnd = random.Random(seed)
+    e = R.Engine(0)
+    e.SetMainInterfaceName("GbE")
+    e.SetVxlanBVIIfName("VXLAN-BVI")
+    e.SetHostInterconnectIfName("VPP-Host")
+    local, ops, pod_ips = {}, [], []
+    for k in range(n_tables - 1):
+        ip = 0x0A0B0000 | (k + 1)
+        pod_ips.append(ip)
+        ifn = "tap%d" % k
+        e.SetPodIfName("ns/p%d" % k, ifn)
+        e.RegisterPod("ns/p%d" % k, W.ip_str(ip), False)
+        local[ip] = ifn
+        outb = []  # from a few pods, a few popular ports: a cross product the node keeps small
+        for _ in range(rnd.randint(1, 3)):
+            r = {"action": rnd.choice([0, 1, 1, 2]), "src": W.ip_str(rnd.choice(pod_ips)) + "/32", "dst": ""}
+            if rnd.random() < 0.7:
+                p = rnd.choice([80, 443, 8080])
+                r[rnd.choice(["tcp", "udp"])] = {"src": [0, 65535], "dst": [p, p]}
+            outb.append(r)
+        outb.append({"action": 0, "src": "", "dst": ""})
+        ops.append(("config/vpp/acls/v2/acl/out-" + ifn, {"name": "out-" + ifn, "rules": outb, "ingress": [],
+                                                         "egress": [ifn]}))
+    glob = [{"action": k % 2, "src": W.ip_str(pod_ips[k]) + "/32", "dst": ""} for k in range(12)]
+    glob.append({"action": 1, "src": "", "dst": ""})
+    ops.append(("config/vpp/acls/v2/acl/g", {"name": "g", "rules": glob, "ingress": [], "egress": ["VXLAN-BVI"]}))
+    e.ApplyTxn(True, ops)
+    return e, (local, []), pod_ips
+
+
+@pytest.mark.parametrize("n_tables", [251, 252, 253, 255, 256])
+def test_uniform_node_at_the_narrow_wide_record_boundary(n_tables):
+    """Table counts either side of the class records' byte-wide table ids (fastpath.cpp
+    build_node: narrow records while every id and the "no ACL" pseudo-table's id fit 0..254,
+    wide 16-bit ids past that). Past 64 tables the common-row marks group 4 tables per bit, and
+    the pseudo-table takes a group of its own, so its id is the table count rounded up to 4:
+    252 tables -> 252 (narrow), 253 -> 256 (wide). The uniform layout either way, and PERPOD /
+    CONN with counters equal to the oracle and the per-table path (check())."""
+    e, local, pod_ips = _many_tables(n_tables, 900 + n_tables)
+    assert e.num_tables() == n_tables
+    ns = e.node_stats()
+    assert ns["uniform"], ns
+    assert ns["wide_records"] == (n_tables > 252), (n_tables, ns["wide_records"])
+    pn, cn = check(e, local, tuples(n_tables, 6007, pod_ips))
+    assert len(set((cn >> 30).tolist())) >= 2
+
+
 def test_node_lists_table_or_records_in_image_or_cross():
     """A node cross entry with dst-specific rules ahead of its verdict resolves them the same
     three ways, all equal to the oracle: by the list-verdict table (default: one read at [list]
