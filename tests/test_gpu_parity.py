@@ -445,6 +445,27 @@ def test_batch_past_32bit_stream_offsets():
     torch.cuda.empty_cache()
 
 
+@pytest.mark.parametrize("n_tables", [252, 253])
+def test_node_kernels_at_the_narrow_wide_record_boundary(n_tables):
+    """The kernels on both sides of the class records' byte-wide table ids (252 tables: narrow
+    records; 253: the "no ACL" pseudo-table's id rounds up to 256, wide records -- see
+    test_node_host.py): PERPOD and CONN with counters equal the host run of the same per-tuple
+    code, which test_node_host.py pins to the oracle; ragged batch, ANY-protocol packets in."""
+    from test_node_host import _many_tables, tuples
+    e, local, pod_ips = _many_tables(n_tables, 900 + n_tables)
+    assert e.node_stats()["wide_records"] == (n_tables > 252)
+    tup = tuples(n_tables, (1 << 16) + 5, pod_ips)
+    b = D.TupleBatch.from_numpy(*tup)
+    for mode in (MODE_PERPOD, MODE_CONN):
+        out = torch.empty(b.n, dtype=torch.int32, device="cuda")
+        cnt = torch.zeros(e.num_counter_slots(), dtype=torch.int64, device="cuda")
+        D.classify(e, mode, -1, b, out, counters=cnt)
+        torch.cuda.synchronize()
+        host, hc = e.debug_classify_host(mode, -1, *tup, counters=True, node=True)
+        assert np.array_equal(out.cpu().numpy().view(np.uint32), host), mode
+        assert np.array_equal(cnt.cpu().numpy(), hc.astype(np.int64)), mode
+
+
 @pytest.mark.parametrize("mode", [MODE_PERPOD, MODE_CONN])
 def test_k8s_object_cluster_gpu_vs_oracle(mode):
     """The cluster given as K8s objects (policy cache -> processor -> configurator -> renderer,
