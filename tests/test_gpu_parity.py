@@ -467,6 +467,36 @@ def test_node_kernels_at_the_narrow_wide_record_boundary(n_tables):
 
 
 @pytest.mark.parametrize("mode", [MODE_PERPOD, MODE_CONN])
+def test_half_cell_histogram_past_0x8000(mode):
+    """Config 8's 202-table set counts into 16-bit LDS cells (k_classify STAGE + 256: its 32-bit
+    histogram would leave LDS for one workgroup per CU). 48M copies of one connection: every
+    workgroup takes each of its slots past 0x8000 several times, each crossing moving 0x8000 to
+    the global counter; the counters equal the host run of that one connection times 48M."""
+    from vpp_amd import workloads as W
+    w = W.config8(0, n_tuples=1 << 10)
+    e = w.engine
+    ips = sorted(w.local_ifs)
+    tup = (np.array([ips[3]], np.uint32), np.array([ips[7]], np.uint32), np.array([40000], np.uint16),
+           np.array([80], np.uint16), np.array([0], np.uint8))
+    host, hc = e.debug_classify_host(mode, -1, *tup, counters=True, node=True)
+    n = 48 << 20
+    b = D.TupleBatch(n, with_sport=True)
+    i32 = lambda x: int(x) - (1 << 32) if int(x) >= (1 << 31) else int(x)  # noqa: E731
+    b.src.fill_(i32(tup[0][0]))
+    b.dst.fill_(i32(tup[1][0]))
+    b.sport.fill_(40000 - 65536)
+    b.dport.fill_(80)
+    b.proto.fill_(0)
+    out = torch.empty(n, dtype=torch.int32, device="cuda")
+    cnt = torch.zeros(e.num_counter_slots(), dtype=torch.int64, device="cuda")
+    D.classify(e, mode, -1, b, out, counters=cnt)
+    torch.cuda.synchronize()
+    assert int((out != i32(host[0])).sum()) == 0
+    assert np.array_equal(cnt.cpu().numpy(), hc.astype(np.int64) * n), np.nonzero(cnt.cpu().numpy() != hc * n)
+    assert int(hc.sum()) >= 1
+
+
+@pytest.mark.parametrize("mode", [MODE_PERPOD, MODE_CONN])
 def test_k8s_object_cluster_gpu_vs_oracle(mode):
     """The cluster given as K8s objects (policy cache -> processor -> configurator -> renderer,
     SURVEY.md §8 f3; 4 namespaces x 30 pods, namespace-wide selectors): 1M device-generated

@@ -297,8 +297,13 @@ constexpr uint32_t kCacheEmpty = 0xFFFFFFFFu;  // slot-cache key of a free cell 
 #define PG_CACHE_PROBES 4
 #endif
 // kHotRegs (kFullOnly builds): slots hot and hot2 are counted in registers
+// kHalf (kFullOnly builds, device.hip STAGE + 256): 16-bit cells, two slots per LDS word (slot s
+// in the half s & 1 of word s >> 1), for node sets whose 32-bit histogram would leave LDS for
+// one workgroup per CU. The increment that takes a cell to 0x8000 moves 0x8000 to the slot's
+// global counter (the cell cannot reach 0x10000 before that lane's subtraction lands: that
+// would take 0x8000 more increments of one slot by one workgroup in between)
 template <bool kFullLds = false, bool kAggGlobal = false, bool kCache = false, bool kFullOnly = false,
-          bool kHotRegs = false>
+          bool kHotRegs = false, bool kHalf = false>
 struct HistT {
     uint32_t* lds;
     unsigned long long* glob;
@@ -325,9 +330,23 @@ struct HistT {
     // one increment of a slot that is never `hot` / `hot2` (the unresolved-interface slot): the
     // full-histogram builds skip the register tests (their loop-invariant results were hoisted
     // out of the CONN loop and spilled, each reload a vmcnt(0) wait)
+#if defined(__HIP_DEVICE_COMPILE__)
+    // one increment of slot in the 16-bit-cell histogram (kHalf)
+    __device__ void half_add(uint32_t slot) const {
+        const uint32_t sh = (slot & 1u) << 4;
+        const uint32_t old = atomicAdd(&lds[slot >> 1], 1u << sh);
+        if (((old >> sh) & 0xFFFFu) == 0x7FFFu) {
+            atomicSub(&lds[slot >> 1], 0x8000u << sh);
+            atomicAdd(&glob[slot], 0x8000ull);
+        }
+    }
+#endif
     PG_HD void inc_cold(uint32_t slot) const {
 #if defined(__HIP_DEVICE_COMPILE__) && !defined(PG_PROBE_NOINC)
-        if constexpr (kFullOnly) {
+        if constexpr (kFullOnly && kHalf) {
+            half_add(slot);
+            return;
+        } else if constexpr (kFullOnly) {
             atomicAdd(&lds[slot], 1u);
             return;
         }
@@ -384,7 +403,13 @@ struct HistT {
     // register-counted slots' offsets and adds at that offset: no mask of the action bits
     PG_HD void inc_w(uint32_t w) const {
 #if defined(__HIP_DEVICE_COMPILE__) && !defined(PG_PROBE_NOINC)
-        if constexpr (kFullOnly && kHotRegs) {
+        if constexpr (kFullOnly && kHotRegs && kHalf) {
+            const uint32_t sl = w & 0x3FFFFFFFu;
+            nhot += sl == hot;
+            nhot2 += sl == hot2;
+            if (sl != hot && sl != hot2) half_add(sl);
+            return;
+        } else if constexpr (kFullOnly && kHotRegs) {
             const uint32_t b = w << 2;
             nhot += b == hot << 2;
             nhot2 += b == hot2 << 2;
@@ -402,7 +427,13 @@ struct HistT {
         if constexpr (kFullOnly && kHotRegs) {  // CONN's two hottest slots in registers
             nhot += slot == hot;
             nhot2 += slot == hot2;
-            if (slot != hot && slot != hot2) atomicAdd(&lds[slot], 1u);
+            if (slot != hot && slot != hot2) {
+                if constexpr (kHalf) half_add(slot);
+                else atomicAdd(&lds[slot], 1u);
+            }
+            return;
+        } else if constexpr (kFullOnly && kHalf) {
+            half_add(slot);
             return;
         } else if constexpr (kFullOnly) {
             atomicAdd(&lds[slot], 1u);
@@ -472,6 +503,17 @@ struct HistT {
     }
     PG_HD void flush_hot() const {  // device: the register count of `hot` into the histogram
 #if defined(__HIP_DEVICE_COMPILE__)
+        if constexpr (kHalf) {  // (16-bit cells) the wave's register counts straight to the global counters
+            uint32_t a = nhot, b = nhot2;
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) a += __shfl_xor(a, o), b += __shfl_xor(b, o);
+            if (__lane_id() == 0) {
+                if (a) atomicAdd(&glob[hot], (unsigned long long)a);
+                if (kHotRegs && b) atomicAdd(&glob[hot2], (unsigned long long)b);
+            }
+            nhot = nhot2 = 0;
+            return;
+        }
         if (kHotRegs && nhot2) {
             atomicAdd(&lds[hot2], nhot2);
             nhot2 = 0;

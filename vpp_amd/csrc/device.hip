@@ -472,6 +472,9 @@ constexpr size_t kLdsPerCU = 160u << 10;
 #ifndef PG_NODE_NOPAIR  // node sets without PAIR tables: the build without PAIR code (STAGE + 32)
 #define PG_NODE_NOPAIR 1
 #endif
+#ifndef PG_NODE_HALF  // uniform node sets whose 32-bit histogram would crowd LDS: 16-bit cells (STAGE + 256)
+#define PG_NODE_HALF 1
+#endif
 #ifndef PG_NODE_FULLH  // node kernels whose LDS histogram holds every slot: the specialised build (STAGE + 16)
 #define PG_NODE_FULLH 1
 #endif
@@ -754,7 +757,9 @@ void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     uint32_t* hist = smem + (STAGE ? stage_words : 0u);
     // node kernels: the LDS histogram, when used, holds every slot (HistT<true>: no window test)
-    HistT<NODE, NODE && MODE == 1 && !FULLH, NODE && !FULLH, FULLH, FULLH && MODE == 2 && PG_CONN_HOT_REGS> h{nullptr,
+    // STAGE_ + 256 (with + 16): the histogram's cells are 16 bits (HistT kHalf)
+    constexpr bool HALF = FULLH && (STAGE_ & 256);
+    HistT<NODE, NODE && MODE == 1 && !FULLH, NODE && !FULLH, FULLH, FULLH && MODE == 2 && PG_CONN_HOT_REGS, HALF> h{nullptr,
                                                                                                   counters};
     DevTable tab0{};
     const uint32_t* blobs = T.blobs;
@@ -793,7 +798,8 @@ void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
     const bool has_hist = COUNT && (!NODE || lds_hist || cache);  // an LDS histogram was allocated
     // STAGE 6 (PG_CANDI_COMPACT): each wave's 256-B scratch after the staged words and histogram
     // (cells + 2 words; a node slot cache would take 2 (cells + 1))
-    const uint32_t hist_words = !has_hist ? 0u : (cache ? 2u * (hist_cells + 1u) : hist_cells + 2u);
+    const uint32_t hist_words = !has_hist ? 0u
+                                : (cache ? 2u * (hist_cells + 1u) : (HALF ? (hist_cells + 1u) / 2u + 1u : hist_cells + 2u));
     uint8_t* const cscr = reinterpret_cast<uint8_t*>(smem + stage_words + hist_words) + (threadIdx.x >> 6) * 256u;
     const uint32_t wn = COUNT ? hist_cells : 0u;
     const uint32_t wbase = (MODE == 0 && wn < T.n_slots) ? min(tab0.rule_base, T.n_slots - wn) : 0u;
@@ -801,7 +807,7 @@ void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
     const uint32_t xslot1 = MODE == 0 ? (tab0.n_rules ? tab0.rule_base + tab0.n_rules - 1u : xslot) : T.slot_unresolved;
     if (COUNT) {
         if (has_hist && !cache)
-            for (uint32_t i = threadIdx.x; i <= wn + 1u; i += BS) hist[i] = 0;
+            for (uint32_t i = threadIdx.x; i < hist_words; i += BS) hist[i] = 0;
         h.lds = lds_hist ? hist : nullptr;
         h.wbase = wbase;
         h.wn = wn;
@@ -992,6 +998,14 @@ void k_classify(DevTableSet T, int32_t t, const uint32_t* __restrict__ src,
     if (COUNT) {
         h.flush_hot();
         __syncthreads();
+        if constexpr (HALF) {  // two 16-bit cells per word: slots 2i and 2i + 1
+            for (uint32_t i = threadIdx.x; i < (wn + 1u) / 2u; i += BS) {
+                const uint32_t v = hist[i];
+                if (v & 0xFFFFu) atomicAdd(&counters[2u * i], (unsigned long long)(v & 0xFFFFu));
+                if ((v >> 16) && 2u * i + 1u < wn) atomicAdd(&counters[2u * i + 1u], (unsigned long long)(v >> 16));
+            }
+            return;
+        }
         for (uint32_t i = threadIdx.x; has_hist && i <= wn + 1u; i += BS) {
             if (cache && i > wn) break;
             const uint32_t v = cache ? hist[wn + 1u + i] : hist[i];
@@ -1250,7 +1264,8 @@ static void launch_one(const DevTableSet& T, const Tuning& tu, int t, const uint
         // The wide sets' images are larger (config 9: 502 tables, 53.8 KB with the common rows),
         // so LDS holds two workgroups per CU where config 3's 41 KB holds three: 768-thread
         // workgroups keep the 24 waves per CU of three 512-thread ones (PG_NODE_WIDE_REC_BS)
-        if constexpr (NODE && (STAGE & 128)) {
+        // (16-bit-cell histogram builds, STAGE + 256: likewise)
+        if constexpr (NODE && (STAGE & (128 | 256))) {
             constexpr int BSW = node_wide<MODE, COUNT, NODE, STAGE>() ? PG_NODE_WIDE_BS : PG_NODE_WIDE_REC_BS;
             return launch_bs<MODE, COUNT, VEC, STAGE, NODE, BSW>(T, tu, t, src, dst, sport, dport, proto, n, out,
                                                                  counters, st, hist, cells, stage, items);
@@ -1307,8 +1322,16 @@ static void launch_classify(const DevTableSet& T, const Tuning& tu, int t, const
     const bool node = MODE != 0 && tu.node_path && T.node.img;
     uint32_t cells = 0;
     size_t hist = 0;
+    // node sets counted into 16-bit cells (k_classify STAGE + 256): the uniform layout, every
+    // slot in the histogram, and a 32-bit histogram that even beside the base image would exceed
+    // the LDS budget of two workgroups per CU (node_common_lds_max)
+    const bool half = PG_NODE_HALF && COUNT && node && PG_NODE_FULLH && T.node.uniform && T.n_slots <= kLdsHistMax - 2u &&
+                      ((size_t)T.n_slots + 2u) * 4 + (size_t)T.node.img_words_base * 4 > tu.node_common_lds_max;
     if (COUNT) {
-        if (T.n_slots <= kLdsHistMax - 2u) {
+        if (half) {
+            cells = T.n_slots;
+            hist = ((size_t)(cells + 1u) / 2u + 1u) * 4;
+        } else if (T.n_slots <= kLdsHistMax - 2u) {
             cells = T.n_slots;
             hist = ((size_t)cells + 2u) * 4;
         } else if (!node) {
@@ -1357,6 +1380,12 @@ static void launch_classify(const DevTableSet& T, const Tuning& tu, int t, const
         auto go1 = [&](auto stage, const DevTableSet& Ts, uint32_t words) {
             constexpr int S = decltype(stage)::value;
             if constexpr (COUNT) {
+                if constexpr ((S & 64) != 0 && PG_NODE_HALF) {
+                    if (full && half)
+                        return launch_one<MODE, COUNT, VEC, S + 16 + 256, true>(Ts, tu, t, src, dst, sport, dport, proto,
+                                                                                n, out, counters, st, hist, cells, words,
+                                                                                items);
+                }
                 if (full)
                     return launch_one<MODE, COUNT, VEC, S + 16, true>(Ts, tu, t, src, dst, sport, dport, proto, n, out,
                                                                       counters, st, hist, cells, words, items);
