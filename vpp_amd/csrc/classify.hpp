@@ -327,9 +327,6 @@ struct HistT {
     // image: config 6 with counters 99 -> 144 Gpps (A/B on MI355X; 1024 cells 129, 4096 128).
     uint32_t* ckey = nullptr;
     uint32_t cmask = 0, cshift = 32;
-    // one increment of a slot that is never `hot` / `hot2` (the unresolved-interface slot): the
-    // full-histogram builds skip the register tests (their loop-invariant results were hoisted
-    // out of the CONN loop and spilled, each reload a vmcnt(0) wait)
 #if defined(__HIP_DEVICE_COMPILE__)
     // one increment of slot in the 16-bit-cell histogram (kHalf)
     __device__ void half_add(uint32_t slot) const {
@@ -341,6 +338,9 @@ struct HistT {
         }
     }
 #endif
+    // one increment of a slot that is never `hot` / `hot2` (the unresolved-interface slot): the
+    // full-histogram builds skip the register tests (their loop-invariant results were hoisted
+    // out of the CONN loop and spilled, each reload a vmcnt(0) wait)
     PG_HD void inc_cold(uint32_t slot) const {
 #if defined(__HIP_DEVICE_COMPILE__) && !defined(PG_PROBE_NOINC)
         if constexpr (kFullOnly && kHalf) {
